@@ -1,0 +1,311 @@
+#!/usr/bin/env python3
+"""Headline benchmark: images/sec of the MoE-fied SD-1.4 denoising step on MI355X (BASELINE.json metric).
+
+Workload (one bench "step" = one batch of B prompts per GPU denoised end to end):
+  SD-1.4 U-Net (859.5M params, synthetic seeded weights), 512^2 -> 4x64x64 latents, 50 DDIM steps, CFG 7.5,
+  relufied + MoE-fied FFNs (expert size 20, top-k 0.2), skilled-expert removal mask active
+  (RemoveExperts: ~10 % of each layer's experts removed for t < 20) driven through the reference receiver API
+  (observe_activation -> forward hooks on all 16 GEGLU FFNs). --mask union additionally applies a 10-concept
+  union Wanda down-projection mask at every step (config 4).
+Multi-GPU: one process per GPU (torchrun), prompts sharded data-parallel (weak scaling, B per GPU), masks
+generated on rank 0 and broadcast once over RCCL; no per-step communication.
+
+Prints ONE JSON line (rank 0). See DESIGN.md §Measurement for the roofline and baseline definitions.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "diffusion-models-moe_amd"), ROOT]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+TFLOP_PER_IMAGE = 81.34       # SD-1.x 512^2, 50 steps, CFG, MoE scoring on
+PEAK_FP16_TFLOPS = 2500.0     # MI355X dense FP16/BF16 MFMA (MI355X_MICROARCH.md, chip table)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=2)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--batch", type=int, default=8, help="prompts per GPU (config 4: 64 prompts / 8 GPUs)")
+    p.add_argument("--inference-steps", type=int, default=50)
+    p.add_argument("--mask", choices=["remove", "union", "none"], default="remove")
+    p.add_argument("--topk", type=float, default=0.2)
+    p.add_argument("--no-roofline", action="store_true")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-evals", type=int, default=2, help="CPU oracle U-Net evaluations to time")
+    p.add_argument("--traffic", type=str, default=None, help="PMC summary json from tools/pmc_traffic.py")
+    return p.parse_args()
+
+
+def setup_dist(n):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, local
+
+
+def synth_expert_lists(num_experts, T, seed=7):
+    """RemoveExperts "Van Gogh" stand-in: ~10 % of E per (t, l) for t < 20 (no real lists offline)."""
+    rng = np.random.default_rng(seed)
+    out = {}
+    for t in range(T):
+        out[t] = {}
+        for l, E in enumerate(num_experts):
+            out[t][l] = sorted(rng.choice(E, size=max(1, E // 10), replace=False).tolist()) if t < 20 else []
+    return out
+
+
+def broadcast_obj(obj, world, rank):
+    if world == 1:
+        return obj
+    lst = [obj if rank == 0 else None]
+    dist.broadcast_object_list(lst, src=0)
+    return lst[0]
+
+
+def build(args, world, rank, dev):
+    from sdmoe.config import UNetConfig
+    from sdmoe.pipeline import StableDiffusionPipeline
+    from moefication.helper import moefy_synthetic
+    from sparsity.relufy_model import find_and_change_geglu
+    from neuron_receivers import RemoveExperts, MOEFy, WandaRemoveNeuronsFast
+
+    cfg = UNetConfig.sd14(64)
+    pipe = StableDiffusionPipeline.synthetic(cfg, seed=0, device=dev, num_inference_steps=args.inference_steps)
+    find_and_change_geglu(pipe.unet)                  # relufied U-Net (config 2/3)
+    moefy_synthetic(pipe, args.topk, 20, seed=0)      # E = 4C/20 experts, k = int(E*topk)
+    geglus = [m for n, m in pipe.unet.named_modules() if n.endswith("ff.net.0")]
+    T = args.inference_steps
+    # masks are produced on rank 0 and broadcast once (RCCL); every rank then holds identical device copies
+    if args.mask == "none":
+        rec = MOEFy(seed=0, store_gates=False)
+    else:
+        lists = broadcast_obj(synth_expert_lists([m.patterns.shape[0] for m in geglus], T) if rank == 0 else None,
+                              world, rank)
+        rec = RemoveExperts(0, None, T, len(geglus), expert_indices=lists, store_gates=False)
+    wanda = None
+    if args.mask == "union":
+        downs = [m for n, m in pipe.unet.named_modules() if n.endswith("ff.net.2")]
+        # 10-concept union, each concept Bernoulli(0.0025) per weight (the union density of ten masks like
+        # weights_320_1280.csv after save_union_experts' 95 % drop): drawn on device, bit-packed on device
+        p_union = 1.0 - (1.0 - 0.0025) ** 10
+        weights8 = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.uint8, device=dev)
+        gen = torch.Generator(device=dev)
+        bits = {}
+        for t in range(T):
+            bits[t] = {}
+            for l, d in enumerate(downs):
+                shape = tuple(d.weight.shape)
+                if rank == 0:
+                    gen.manual_seed(1000 * t + l)
+                    m = torch.rand(shape, generator=gen, device=dev) < p_union
+                    b = (m.view(shape[0], shape[1] // 8, 8).to(torch.uint8) * weights8).sum(-1, dtype=torch.uint8)
+                else:
+                    b = torch.empty((shape[0], shape[1] // 8), dtype=torch.uint8, device=dev)
+                if world > 1:
+                    dist.broadcast(b, src=0)
+                bits[t][l] = b.contiguous()
+        wanda = WandaRemoveNeuronsFast.from_packed(0, {t: {l: np.zeros((1, 1), np.uint8) for l in range(len(downs))}
+                                                       for t in range(T)}, T, len(downs), store_gates=False)
+        for t in range(T):
+            for l in range(len(downs)):
+                wanda._dev[(t, l)] = bits[t][l]
+    return cfg, pipe, rec, wanda
+
+
+class KernelTimer:
+    """HIP-event timing of every launch of one kernel family on the stream it is launched on."""
+
+    def __init__(self, family):
+        self.family = family
+        self.pairs = []
+        self.flops = 0.0
+        self.bytes = 0.0
+        self.active = False
+
+    def wrap(self, ops_mod):
+        orig = getattr(ops_mod, self.family)
+        timer = self
+
+        def wrapped(*a, **k):
+            if not timer.active:
+                return orig(*a, **k)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            out = orig(*a, **k)
+            e.record()
+            timer.pairs.append((s, e))
+            timer.account(a, k, out)
+            return out
+        setattr(ops_mod, self.family, wrapped)
+        import sdmoe.unet as U
+        if hasattr(U.ops, self.family):
+            setattr(U.ops, self.family, wrapped)
+
+    def account(self, a, k, out):
+        x, w = a[0], a[4]
+        cin_real = 4 if getattr(w, "_sdmoe_conv_in", False) else x.shape[1]  # conv_in: 4 real of 64 padded
+        M = out.shape[0]
+        N = 4 if getattr(w, "_sdmoe_conv_out", False) else w.shape[0]  # conv_out: 4 real of 8 padded
+        self.flops += 2.0 * M * N * 9 * cin_real
+        self.bytes += (x.shape[0] * x.shape[1] + w.numel() + out.numel()) * 2.0
+
+    def result(self):
+        torch.cuda.synchronize()
+        ms = sum(s.elapsed_time(e) for s, e in self.pairs)
+        n = len(self.pairs)
+        return n, ms, self.flops
+
+
+def cpu_baseline(args):
+    """The oracle (fp32 CPU restatement of the reference path, incl. the hook's projection recompute) timed on
+    this host's cores for a bounded sample: `cpu_evals` CFG U-Net evaluations at B=1 (one denoising step each)."""
+    from oracle.unet_ref import UNetRef
+    from oracle import hooks_ref as H
+    from sdmoe.config import UNetConfig
+    from sdmoe.weights import make_state_dict
+    from sdmoe.pipeline import prompt_embedding
+    from moefication.helper import balanced_random_labels
+    import torch.nn.functional as F
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    cfg = UNetConfig.sd14(64)
+    ref = UNetRef(make_state_dict(cfg, 0), cfg)
+    layers = []
+    for i, (_, C) in enumerate(cfg.geglu_layers()):
+        lab = balanced_random_labels(4 * C, 20, i)
+        E = 4 * C // 20
+        layers.append((H.patterns_from_labels(lab), int(E * args.topk)))
+    rng = np.random.default_rng(7)
+
+    def hook(layer, x, w, b):
+        F.linear(x, w, b)  # the module's own GEGLU forward, which the reference hook then recomputes (K1)
+        P, k = layers[layer]
+        ids = rng.choice(P.shape[0], size=max(1, P.shape[0] // 10), replace=False).tolist()
+        return H.geglu_hook(x, w, b, P, k, "relu", removed=ids)[0]
+
+    x = torch.randn(2, 4, 64, 64)
+    ctx = torch.stack([prompt_embedding("", 768), prompt_embedding("a painting", 768)])
+    with torch.no_grad():
+        ref(x, 981.0, ctx, ff_hook=hook)  # warm-up (allocator, threads)
+        t0 = time.perf_counter()
+        for _ in range(args.cpu_evals):
+            ref(x, 981.0, ctx, ff_hook=hook)
+        dt = (time.perf_counter() - t0) / args.cpu_evals
+    per_image = dt * args.inference_steps
+    return {"value": 1.0 / per_image, "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{args.cpu_evals} CFG U-Net evals (B=1, 2x4x64x64, MoE routing + removal hooks) at "
+                      f"{dt:.2f} s each, x{args.inference_steps} steps per image"}
+
+
+def main():
+    args = parse()
+    world, rank, local = setup_dist(args.gpus)
+    dev = f"cuda:{local}" if world > 1 else "cuda:0"
+    from sdmoe import ops, _lib
+    _lib.load()
+    cfg, pipe, rec, wanda = build(args, world, rank, dev)
+    # global prompt list: rank r takes its contiguous shard (per-prompt seeds use the global index)
+    prompts = [f"synthetic prompt {i}" for i in range(world * args.batch)]
+    mine = prompts[rank * args.batch:(rank + 1) * args.batch]
+
+    timer = KernelTimer("conv3x3")
+    if not args.no_roofline:
+        timer.wrap(ops)
+    pipe.unet.conv_in.weight._sdmoe_conv_in = True
+    pipe.unet.conv_out.weight._sdmoe_conv_out = True
+
+    pipe.prompt_offset = rank * args.batch  # global prompt index of this rank's first prompt
+
+    def one_step():
+        """One batch through the reference receiver API: observe_activation(pipe, prompts)."""
+        hooks = []
+        if wanda is not None:
+            wanda.reset_time_layer()
+            hooks = wanda.register_hooks(pipe)
+        try:
+            if hasattr(rec, "reset_time_layer"):
+                rec.reset_time_layer()
+            out, _ = rec.observe_activation(pipe, mine)
+        finally:
+            if wanda is not None:
+                wanda.remove_hooks(hooks)
+        return out
+
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    timer.active = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        imgs = one_step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    timer.active = False
+    if world > 1:
+        dist.barrier()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    finite = all(bool(torch.isfinite(x).all()) for x in imgs)
+    images = world * args.batch * args.steps
+    value = images / elapsed
+
+    roof = None
+    if not args.no_roofline:
+        n, ms, flops = timer.result()
+        if n:
+            achieved = flops / (ms / 1e3) / 1e12
+            traffic = None
+            if args.traffic and os.path.exists(args.traffic):
+                traffic = json.load(open(args.traffic)).get("bytes_per_launch")
+            roof = {"bound": "mfma", "kernel": "sdmoe conv3x3 implicit-GEMM (gemm_kernel<...,CONV=true,...>)",
+                    "achieved": round(achieved, 1), "peak": PEAK_FP16_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(achieved / PEAK_FP16_TFLOPS, 4), "traffic": traffic,
+                    "launches": n, "avg_launch_ms": round(ms / n, 4),
+                    "algorithmic_flop_per_launch": round(flops / n)}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args)
+    if rank == 0:
+        line = {
+            "metric": "images/sec SD-1.4 512² 50-step DDIM, expert mask on; 1→8 GPU scaling",
+            "value": round(value, 4), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp16", "data": "synthetic",
+            "config": {"workload": f"SD-1.4 MoE-fied (relu, top-k {args.topk}, expert 20) + "
+                                   f"{'RemoveExperts skilled-expert mask' if args.mask != 'none' else 'no mask'}"
+                                   f"{' + union Wanda mask' if args.mask == 'union' else ''}, 512^2 "
+                                   f"(4x64x64 latents), {args.inference_steps} DDIM steps, CFG 7.5",
+                       "prompts_per_gpu": args.batch, "global_batch": world * args.batch,
+                       "parallelism": f"dp{world}"},
+            "step_mfma_frac": round(value / world * TFLOP_PER_IMAGE / PEAK_FP16_TFLOPS, 4),
+            "roofline": roof, "cpu_baseline": cpu, "outputs_finite": finite,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,67 @@
+// Shared device helpers for the sdmoe gfx950 (CDNA4) kernels.
+// All kernels are written for wave64 and the gfx950 MFMA set; nothing here is portable on purpose.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef _Float16 half_t;
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+typedef float float4v __attribute__((ext_vector_type(4)));
+typedef short short4v __attribute__((ext_vector_type(4)));
+typedef unsigned int uint4v __attribute__((ext_vector_type(4)));
+
+#define SDMOE_DEV __device__ __forceinline__
+
+// Status codes returned by every C-ABI entry point (0 = ok, >0 = hipError_t, <0 = argument error).
+enum {
+  SDMOE_OK = 0,
+  SDMOE_EARG = -1,     // null pointer / bad size
+  SDMOE_ESHAPE = -2,   // unsupported shape (alignment / divisibility)
+  SDMOE_EUNSUP = -3,   // unsupported mode
+};
+
+#define SDMOE_CHECK_LAUNCH()                          \
+  do {                                                \
+    hipError_t _e = hipGetLastError();                \
+    if (_e != hipSuccess) return (int)_e;             \
+  } while (0)
+
+SDMOE_DEV float4v mfma16x16x32(half8 a, half8 b, float4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+SDMOE_DEV float silu_f(float x) { return x / (1.0f + __expf(-x)); }
+SDMOE_DEV float gelu_erf_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+
+SDMOE_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+SDMOE_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Activation kinds shared by the host ABI (include/sdmoe.h).
+enum { ACT_NONE = 0, ACT_SILU = 1, ACT_GELU = 2, ACT_RELU = 3 };
+
+SDMOE_DEV float apply_act(float v, int act) {
+  if (act == ACT_SILU) return silu_f(v);
+  if (act == ACT_GELU) return gelu_erf_f(v);
+  if (act == ACT_RELU) return v > 0.f ? v : 0.f;
+  return v;
+}
+
+// XCD-aware bijective remap of a 1-D block id (8 XCDs, round-robin dispatch):
+// consecutive logical tiles land on the same XCD so they share its L2.
+SDMOE_DEV int xcd_remap(int bid, int nblocks) {
+  const int nx = 8;
+  if (nblocks < nx) return bid;
+  int q = nblocks / nx, r = nblocks % nx;
+  int xcd = bid % nx, idx = bid / nx;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}

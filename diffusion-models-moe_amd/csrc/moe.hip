@@ -1,0 +1,166 @@
+// MoE-fied GEGLU routing for gfx950: the hot arithmetic of the reference receivers
+//   MOEFy.hook_fn            (neuron_receivers/moefy.py:10-27)
+//   RemoveExperts.hook_fn    (neuron_receivers/remove_skilled_experts.py:24-55)
+// restated as ONE kernel over the GEGLU projection output Y = proj(x) = [value | gate] (diffusers GEGLU:
+// first half value, second half gate, moe_utils.py:68-72):
+//   g      = act(gate)                   (exact-erf GELU, or ReLU for the relufied U-Net), rounded to fp16
+//   score  = g @ patterns^T              per-expert fp32 sum over its neurons in neuron order, rounded to fp16
+//                                        (removed experts: patterns row zeroed -> score exactly 0)
+//   sel    = top-k(score)                wave-wide 16-bit radix select on order-preserving fp16 keys,
+//                                        ties at the k-th value broken toward the LOWEST expert id
+//   keep_n = sel[label[n]] && !removed[label[n]]   (embedding(labels, patterns').sum(-2) != 0)
+//   out    = keep ? fp16(value * g) : 0             (gate[mask == 0] = 0; hidden_states * gate)
+// One wave per token, no [tokens, k, 4C] temporaries (reference K5), no host sync (reference K8 is an optional
+// gate_out capture written on device).
+#include "common.h"
+#include "../../include/sdmoe.h"
+
+namespace {
+
+struct RouteParams {
+  const half_t* Y; long ldy;
+  int M, F, E, k, act;
+  const int* labels;        // [F] expert id of each inner neuron
+  const int* e_off;         // [E+1] CSR offsets into e_nid
+  const int* e_nid;         // [F] neuron ids grouped by expert, ascending within an expert
+  const uint32_t* removed;  // [ceil(E/32)] or null
+  half_t* out; long ldo;
+  half_t* gate_out; long ldg;
+  uint32_t* sel_out;        // [M][ceil(E/32)] or null (top-k result, before the removal mask)
+  half_t* score_out;        // [M][E] or null
+};
+
+SDMOE_DEV uint32_t order_key(half_t s) {
+  unsigned short u = __builtin_bit_cast(unsigned short, s);
+  if ((u & 0x7fff) == 0) u = 0;  // -0 == +0 for topk
+  return (u & 0x8000) ? (uint32_t)(~u & 0xffff) : (uint32_t)(u | 0x8000);
+}
+
+template <int SLOTS>
+__global__ __launch_bounds__(256) void geglu_route_kernel(RouteParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int F = p.F;
+  half_t* gact = reinterpret_cast<half_t*>(smem) + wave * F;
+  uint32_t* selw = reinterpret_cast<uint32_t*>(reinterpret_cast<half_t*>(smem) + 4 * F) + wave * 8;
+  const int m = blockIdx.x * 4 + wave;
+  const bool live = m < p.M;
+  const int mm = live ? m : 0;
+  const half_t* yrow = p.Y + (long)mm * p.ldy;
+  const int nch = F >> 3;
+
+  // 1) activated gate -> LDS (fp16, as the reference's module.gelu(gate) on an fp16 tensor)
+  for (int c = lane; c < nch; c += 64) {
+    half8 v = *reinterpret_cast<const half8*>(yrow + F + 8 * c);
+    half8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (half_t)apply_act((float)v[j], p.act);
+    *reinterpret_cast<half8*>(gact + 8 * c) = o;
+  }
+  __syncthreads();
+
+  const int nw = (p.E + 31) >> 5;
+  if (p.E > 0) {
+    // 2) expert scores
+    uint32_t key[SLOTS];
+    bool valid[SLOTS];
+#pragma unroll
+    for (int i = 0; i < SLOTS; ++i) {
+      const int e = lane + 64 * i;
+      valid[i] = e < p.E;
+      half_t sc = (half_t)0.f;
+      if (valid[i]) {
+        float acc = 0.f;
+        const int j0 = p.e_off[e], j1 = p.e_off[e + 1];
+        for (int j = j0; j < j1; ++j) acc += (float)gact[p.e_nid[j]];
+        sc = (half_t)acc;
+        if (p.removed && ((p.removed[e >> 5] >> (e & 31)) & 1u)) sc = (half_t)0.f;
+        if (p.score_out && live) p.score_out[(long)m * p.E + e] = sc;
+      }
+      key[i] = valid[i] ? order_key(sc) : 0u;
+    }
+    // 3) radix select of the k-th largest key
+    uint32_t T = 0;
+    for (int bit = 15; bit >= 0; --bit) {
+      const uint32_t cand = T | (1u << bit);
+      int cnt = 0;
+#pragma unroll
+      for (int i = 0; i < SLOTS; ++i) cnt += __popcll(__ballot(valid[i] && key[i] >= cand));
+      if (cnt >= p.k) T = cand;
+    }
+    int gt = 0;
+#pragma unroll
+    for (int i = 0; i < SLOTS; ++i) gt += __popcll(__ballot(valid[i] && key[i] > T));
+    const int need = p.k - gt;
+    const unsigned long long below = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
+    int rank_base = 0;
+#pragma unroll
+    for (int i = 0; i < SLOTS; ++i) {
+      const bool tie = valid[i] && key[i] == T;
+      const unsigned long long tm = __ballot(tie);
+      const bool sel = p.k > 0 && valid[i] && (key[i] > T || (tie && rank_base + __popcll(tm & below) < need));
+      rank_base += __popcll(tm);
+      const unsigned long long sm = __ballot(sel);
+      if (lane == 0) {
+        if (2 * i < 8) selw[2 * i] = (uint32_t)sm;
+        if (2 * i + 1 < 8) selw[2 * i + 1] = (uint32_t)(sm >> 32);
+      }
+    }
+    __syncthreads();
+    if (p.sel_out && live && lane < nw) p.sel_out[(long)m * nw + lane] = selw[lane];
+    if (p.removed && lane < nw) selw[lane] &= ~p.removed[lane];
+    __syncthreads();
+  } else {
+    __syncthreads();
+    __syncthreads();
+  }
+
+  // 4) gated output
+  if (!live) return;
+  for (int c = lane; c < nch; c += 64) {
+    half8 hv = *reinterpret_cast<const half8*>(yrow + 8 * c);
+    half8 ga = *reinterpret_cast<const half8*>(gact + 8 * c);
+    half8 o, go;
+    if (p.E > 0) {
+      const int4* lp = reinterpret_cast<const int4*>(p.labels + 8 * c);
+      int4 l0 = lp[0], l1 = lp[1];
+      int lab[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const bool keep = (selw[lab[j] >> 5] >> (lab[j] & 31)) & 1u;
+        go[j] = keep ? ga[j] : (half_t)0.f;
+        o[j] = keep ? (half_t)((float)hv[j] * (float)ga[j]) : (half_t)0.f;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { go[j] = ga[j]; o[j] = (half_t)((float)hv[j] * (float)ga[j]); }
+    }
+    *reinterpret_cast<half8*>(p.out + (long)m * p.ldo + 8 * c) = o;
+    if (p.gate_out) *reinterpret_cast<half8*>(p.gate_out + (long)m * p.ldg + 8 * c) = go;
+  }
+}
+
+}  // namespace
+
+extern "C" int sdmoe_geglu_route(const void* Y, long ldy, int M, int F, int E, int k, int act, const int* labels,
+                                 const int* e_off, const int* e_nid, const unsigned* removed_bits, void* out,
+                                 long ldo, void* gate_out, long ldg, unsigned* sel_out, void* score_out,
+                                 void* stream) {
+  if (!Y || !out || M < 0 || F <= 0 || E < 0) return SDMOE_EARG;
+  if (M == 0) return SDMOE_OK;
+  if (F % 8 || ldy % 8 || ldo % 8 || (gate_out && ldg % 8)) return SDMOE_ESHAPE;
+  if (E > 256) return SDMOE_EUNSUP;
+  if (E > 0 && (!labels || !e_off || !e_nid || k < 0 || k > E)) return SDMOE_EARG;
+  if (!(act == ACT_GELU || act == ACT_RELU || act == ACT_NONE || act == ACT_SILU)) return SDMOE_EUNSUP;
+  RouteParams p{(const half_t*)Y, ldy, M, F, E, k, act, labels, e_off, e_nid, removed_bits,
+                (half_t*)out, ldo, (half_t*)gate_out, ldg, sel_out, (half_t*)score_out};
+  const size_t smem = (size_t)4 * F * sizeof(half_t) + 4 * 8 * sizeof(uint32_t);
+  if (smem > 160 * 1024) return SDMOE_ESHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  const int blocks = (M + 3) / 4;
+  if (E <= 64) geglu_route_kernel<1><<<blocks, 256, smem, s>>>(p);
+  else if (E <= 128) geglu_route_kernel<2><<<blocks, 256, smem, s>>>(p);
+  else geglu_route_kernel<4><<<blocks, 256, smem, s>>>(p);
+  SDMOE_CHECK_LAUNCH();
+  return SDMOE_OK;
+}

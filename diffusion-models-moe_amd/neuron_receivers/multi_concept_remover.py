@@ -1,0 +1,72 @@
+"""MultiConceptRemoverWanda — drop-in for neuron_receivers/multi_concept_remover.py:13-99 (config 4 union).
+
+One WandaRemoveNeuronsFast per concept plus a union remover whose (t, l) masks are the element-wise OR of the
+selected concepts' masks (:43-53). The snapshot's union step crashes (App. A #6); this restates the intended
+OR, done directly on the bit-packed masks (bitwise OR of packed bytes == element-wise OR of the masks).
+Image stitching (:83-99) is outside this tier: remove_concepts returns the latents.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+from neuron_receivers.base_receiver import GEGLU
+from neuron_receivers.remove_wanda_neurons_fast import WandaRemoveNeuronsFast
+
+
+class MultiConceptRemoverWanda:
+    def __init__(self, root, seed, T, n_layers, replace_fn=GEGLU, keep_nsfw=False, remove_timesteps=None,
+                 weights_shape=None, concepts_to_remove=None, wanda_thr=0.05, removers=None):
+        self.concepts_to_remove = list(concepts_to_remove or [])
+        self.seed, self.T, self.n_layers = seed, T, n_layers
+        if removers is not None:
+            self.removers = dict(removers)
+        else:
+            self.removers = {}
+            for concept in self.concepts_to_remove:
+                thr = wanda_thr[concept] if isinstance(wanda_thr, dict) else wanda_thr
+                path = os.path.join(root % (seed, concept), f'skilled_neuron_wanda/{thr}')
+                self.removers[concept] = WandaRemoveNeuronsFast(
+                    seed=seed, path_expert_indx=path, T=T, n_layers=n_layers, replace_fn=replace_fn,
+                    keep_nsfw=keep_nsfw, remove_timesteps=remove_timesteps, weights_shape=weights_shape)
+        first = next(iter(self.removers.values()))
+        zeros = {t: {l: np.zeros_like(first.mask_bits[t][l]) for l in range(n_layers)} for t in range(T)}
+        self.union_neuron_remover = WandaRemoveNeuronsFast.from_packed(seed, zeros, T, n_layers, replace_fn=replace_fn,
+                                                                       keep_nsfw=keep_nsfw)
+
+    def reset_union_remover(self):
+        u = self.union_neuron_remover
+        u.reset_time_layer()
+        for t in range(self.T):
+            for l in range(self.n_layers):
+                u.set_mask_bits(t, l, np.zeros_like(u.mask_bits[t][l]))
+
+    def handle_multiple_concepts(self, concepts):
+        u = self.union_neuron_remover
+        for c in concepts:
+            self.removers[c].reset_time_layer()
+            for t in range(self.T):
+                for l in range(self.n_layers):
+                    u.set_mask_bits(t, l, np.bitwise_or(u.mask_bits[t][l], self.removers[c].mask_bits[t][l]))
+
+    def remove_concepts(self, model, prompt, concepts):
+        """Returns (latents with the union removed, latents without removal, per-concept latents)."""
+        if len(concepts) == 0:
+            return model(prompt).images[0], None
+        singles = []
+        if len(concepts) > 1:
+            self.handle_multiple_concepts(concepts)
+            self.union_neuron_remover.reset_time_layer()
+            out_removal, _ = self.union_neuron_remover.observe_activation(model, prompt)
+            for c in concepts:
+                self.removers[c].reset_time_layer()
+                singles.append(self.removers[c].observe_activation(model, prompt)[0])
+        else:
+            self.removers[concepts[0]].reset_time_layer()
+            out_removal, _ = self.removers[concepts[0]].observe_activation(model, prompt)
+        torch.manual_seed(self.seed)
+        np.random.seed(self.seed)
+        out_pre = model(prompt).images[0]
+        return out_removal, out_pre, (singles if singles else None)

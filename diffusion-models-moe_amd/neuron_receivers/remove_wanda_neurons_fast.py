@@ -1,0 +1,119 @@
+"""WandaRemoveNeuronsFast — drop-in for neuron_receivers/remove_wanda_neurons_fast.py:12-167 (configs 4-5).
+
+linear_hook_fn (:69-83) semantics kept: at every hooked `ff.net.2` call, y = F.linear(x, W * (1 - M[t][l]), b),
+then the (t, l) counter advances. The mask applies at every step (App. A #8); `remove_timesteps` and
+`weights_shape` are accepted (callers pass them, App. A #5) — weights_shape is used for JSON index masks,
+remove_timesteps is stored but, as in the reference's Fast receiver, not consulted.
+MI355X layout: masks are bit-packed [C, 4C/8] and uploaded once (all (t, l): 316 MB for SD-1.4 at T=51, vs
+~20 GB as dense int64 in the reference); the GEMM zeroes masked weights while staging W tiles, so there is no
+per-call host->device mask copy, no W.clone() and no second GEMM (reference K9).
+The GEGLU variant hook_fn (:31-61, mask over the gate half of proj.weight) uses the same bitmask path.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from sdmoe import mask_io, ops
+from sdmoe.unet import LoRACompatibleLinear
+
+from neuron_receivers.base_receiver import GEGLU
+from neuron_receivers.predictivity import NeuronPredictivity
+
+
+class WandaRemoveNeuronsFast(NeuronPredictivity):
+    def __init__(self, seed, path_expert_indx, T, n_layers, replace_fn=GEGLU, keep_nsfw=False, hook_module='unet',
+                 remove_timesteps=None, weights_shape=None, masks=None, **kw):
+        super().__init__(seed, T, n_layers, replace_fn, keep_nsfw, hook_module, **kw)
+        self.remove_timesteps = remove_timesteps
+        self.weights_shape = weights_shape
+        # mask_bits[t][l]: np.uint8 [C, 4C/8] (host); device copies made once in prepare()
+        self.mask_bits = {}
+        for i in range(T):
+            self.mask_bits[i] = {}
+            for j in range(n_layers):
+                if masks is not None:
+                    bits = mask_io.pack_mask(masks[i][j])
+                else:
+                    bits = mask_io.load_wanda_mask(path_expert_indx, i, j, weights_shape)
+                self.mask_bits[i][j] = bits
+        self.timestep = 0
+        self.layer = 0
+        self.gates = []
+        self._dev = {}
+
+    @classmethod
+    def from_packed(cls, seed, packed, T, n_layers, **kw):
+        """Build from already bit-packed masks packed[t][l] (np.uint8 [C, 4C/8])."""
+        obj = cls.__new__(cls)
+        NeuronPredictivity.__init__(obj, seed, T, n_layers, kw.pop("replace_fn", GEGLU), kw.pop("keep_nsfw", False),
+                                    kw.pop("hook_module", 'unet'), **kw)
+        obj.remove_timesteps, obj.weights_shape = None, None
+        obj.mask_bits = {t: {l: np.asarray(packed[t][l], dtype=np.uint8) for l in range(n_layers)} for t in range(T)}
+        obj.timestep, obj.layer, obj.gates, obj._dev = 0, 0, [], {}
+        return obj
+
+    def dense_mask(self, t, l):
+        bits = self.mask_bits[t][l]
+        return mask_io.unpack_mask(bits, bits.shape[-1] * 8)
+
+    def set_mask_bits(self, t, l, bits):
+        self.mask_bits[t][l] = np.asarray(bits, dtype=np.uint8)
+        self._dev.pop((t, l), None)
+
+    def device_bits(self, t, l, device):
+        d = self._dev.get((t, l))
+        if d is None:
+            d = self._dev[(t, l)] = torch.from_numpy(np.ascontiguousarray(self.mask_bits[t][l])).to(device)
+        return d
+
+    def hook_modules(self, model):
+        if self.hook_module != 'unet':
+            raise NotImplementedError("text-encoder hooks are outside this tier")
+        # remove_wanda_neurons_fast.py:107-112: LoRACompatibleLinear, 'ff.net' in name, not a '.proj'
+        return [(n, m) for n, m in model.unet.named_modules()
+                if isinstance(m, LoRACompatibleLinear) and 'ff.net' in n and 'proj' not in n]
+
+    def prepare(self, model):
+        mods = [m for _, m in self.hook_modules(model)]
+        dev = mods[0].weight.device
+        for t in range(self.T):
+            for l in range(self.n_layers):
+                self.device_bits(t, l, dev)
+
+    def register_hooks(self, model, bboxes=None):
+        return [self._register(m, self.linear_hook_fn) for _, m in self.hook_modules(model)]
+
+    def observe_activation(self, model, ann, bboxes=None):
+        self.prepare(model)
+        return super().observe_activation(model, ann, bboxes)
+
+    def linear_hook_fn(self, module, input, output):
+        x = input[0]
+        bits = self.device_bits(self.timestep, self.layer, module.weight.device)
+        if bits.shape[0] != module.weight.shape[0] or bits.shape[1] * 8 != module.weight.shape[1]:
+            raise ValueError(f"mask ({self.timestep},{self.layer}) shape {tuple(bits.shape)} does not match weight "
+                             f"{tuple(module.weight.shape)}")
+        y = module.run(x.reshape(-1, x.shape[-1]), wmask_bits=bits)
+        self.update_time_layer()
+        return y.view(*x.shape[:-1], module.weight.shape[0])
+
+    def hook_fn(self, module, input, output):
+        """GEGLU variant (:31-61): mask M [4C, C] over the gate half of proj.weight, dense value*act(gate)."""
+        bits = self.device_bits(self.timestep, self.layer, module.proj.weight.device)
+        key = ("gate_full", self.timestep, self.layer)
+        full = self._dev.get(key)
+        if full is None:
+            F4, Kb = bits.shape
+            full = torch.cat([torch.zeros((F4, Kb), dtype=torch.uint8, device=bits.device), bits], 0).contiguous()
+            self._dev[key] = full
+        x = input[0]
+        y = module.proj.run(x.reshape(-1, x.shape[-1]), wmask_bits=full)
+        gate = torch.empty((y.shape[0], module.inner_dim), dtype=torch.float16, device=y.device) \
+            if self.store_gates else None
+        from sdmoe.unet import act_code
+        out = ops.geglu_route(y, None, act_code(module.gelu), gate_out=gate)
+        if self.store_gates:
+            self.gates.append(gate.view(*x.shape[:-1], -1).cpu())
+        self.update_time_layer()
+        return out.view(*x.shape[:-1], module.inner_dim)

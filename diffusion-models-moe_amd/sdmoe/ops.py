@@ -1,0 +1,252 @@
+"""Torch-facing wrappers of the HIP kernels (libsdmoe_hip.so).
+
+PyTorch is used only for device memory and streams: every op here validates its operands, hands raw device
+pointers plus sizes to the C ABI (include/sdmoe.h) on the current HIP stream, and returns. Nothing falls back
+to an eager or CPU implementation; a missing library or a non-GPU tensor raises.
+
+Activations are 2-D row-major views [rows, channels] whose row stride may exceed the channel count (channel
+slices of a concatenation buffer, fused QKV outputs); spatial tensors are NHWC flattened to [images*H*W, C].
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+ACT_NONE, ACT_SILU, ACT_GELU, ACT_RELU = 0, 1, 2, 3
+ACT_BY_NAME = {"none": ACT_NONE, "silu": ACT_SILU, "gelu": ACT_GELU, "relu": ACT_RELU}
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _rows(t: torch.Tensor, name: str):
+    """(data_ptr, row stride) of a 2-D row-major fp16 device view."""
+    if t.dim() != 2:
+        raise ValueError(f"{name}: expected a 2-D [rows, channels] view, got shape {tuple(t.shape)}")
+    if not t.is_cuda:
+        raise _lib.SdmoeError(f"{name}: tensor is not on a GPU device; sdmoe has no CPU path")
+    if t.dtype != torch.float16:
+        raise TypeError(f"{name}: expected float16, got {t.dtype}")
+    if t.stride(1) != 1 and t.shape[1] > 1:
+        raise ValueError(f"{name}: inner dimension must be contiguous")
+    return t.data_ptr(), t.stride(0)
+
+
+def _dev(t: torch.Tensor, name: str, dtype=torch.float16):
+    if not t.is_cuda:
+        raise _lib.SdmoeError(f"{name}: tensor is not on a GPU device; sdmoe has no CPU path")
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: expected a contiguous tensor")
+    return t.data_ptr()
+
+
+def linear(x, w, bias=None, *, out=None, residual=None, act=ACT_NONE, coladd=None, coladd_bstride=0,
+           rows_per_batch=0, gn=None, wmask_bits=None):
+    """out = act(GN?(x) @ w.T + bias + coladd) + residual.  w: [N, K] fp16 (nn.Linear layout).
+    gn = (scale, shift, silu) fp32 [images, K] per-(image, channel) GroupNorm apply fused into the load."""
+    lib = _lib.load()
+    xp, lda = _rows(x, "x")
+    M, K = x.shape
+    N = w.shape[0]
+    if w.shape[1] != K:
+        raise ValueError(f"linear: weight {tuple(w.shape)} does not match input K={K}")
+    wp = _dev(w, "w")
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float16, device=x.device)
+    op, ldc = _rows(out, "out")
+    rp, ldr = (None, 0) if residual is None else _rows(residual, "residual")
+    sc = sh = None
+    silu = 0
+    if gn is not None:
+        sc, sh, silu = gn[0].data_ptr(), gn[1].data_ptr(), int(bool(gn[2]))
+    st = lib.sdmoe_linear(xp, lda, wp, w.stride(0), _ptr(bias), _ptr(coladd), coladd_bstride, rows_per_batch,
+                          rp, ldr, op, ldc, M, N, K, act, sc, sh, silu, _ptr(wmask_bits), _stream())
+    _lib.check(st, "sdmoe_linear")
+    return out
+
+
+def conv3x3(x, nimg, H, W, w, bias=None, *, stride=1, upsample=False, out=None, residual=None, act=ACT_NONE,
+            coladd=None, coladd_bstride=0, gn=None):
+    """3x3 conv (pad 1) on NHWC x viewed as [nimg*H*W, Cin]; w: [Cout, 3, 3, Cin] fp16."""
+    lib = _lib.load()
+    xp, ldx = _rows(x, "x")
+    Cin = x.shape[1]
+    Cout = w.shape[0]
+    if tuple(w.shape[1:]) != (3, 3, Cin):
+        raise ValueError(f"conv3x3: weight {tuple(w.shape)} does not match Cin={Cin}")
+    if x.shape[0] != nimg * H * W:
+        raise ValueError("conv3x3: rows != nimg*H*W")
+    if upsample:
+        OH, OW = 2 * H, 2 * W
+    else:
+        OH, OW = (H - 1) // stride + 1, (W - 1) // stride + 1
+    if out is None:
+        out = torch.empty((nimg * OH * OW, Cout), dtype=torch.float16, device=x.device)
+    op, ldy = _rows(out, "out")
+    rp, ldr = (None, 0) if residual is None else _rows(residual, "residual")
+    sc = sh = None
+    silu = 0
+    if gn is not None:
+        sc, sh, silu = gn[0].data_ptr(), gn[1].data_ptr(), int(bool(gn[2]))
+    st = lib.sdmoe_conv3x3(xp, ldx, nimg, H, W, Cin, _dev(w, "w"), _ptr(bias), _ptr(coladd), coladd_bstride, rp, ldr,
+                           op, ldy, Cout, stride, int(bool(upsample)), act, sc, sh, silu, _stream())
+    _lib.check(st, "sdmoe_conv3x3")
+    return out
+
+
+def groupnorm_stats(x, nimg, HW, gamma, beta, eps, groups=32):
+    """Per-(image, channel) fp32 (scale, shift) of GroupNorm(groups) over x viewed as [nimg*HW, C]."""
+    lib = _lib.load()
+    xp, ldx = _rows(x, "x")
+    C = x.shape[1]
+    scale = torch.empty((nimg, C), dtype=torch.float32, device=x.device)
+    shift = torch.empty((nimg, C), dtype=torch.float32, device=x.device)
+    ws = torch.empty((nimg * groups * 64 * 2,), dtype=torch.float32, device=x.device)
+    st = lib.sdmoe_groupnorm_stats(xp, ldx, nimg, HW, C, groups, _dev(gamma, "gamma"), _dev(beta, "beta"),
+                                   float(eps), scale.data_ptr(), shift.data_ptr(), ws.data_ptr(), ws.numel(),
+                                   _stream())
+    _lib.check(st, "sdmoe_groupnorm_stats")
+    return scale, shift
+
+
+def layernorm(x, gamma, beta, eps=1e-5, out=None):
+    lib = _lib.load()
+    xp, ldx = _rows(x, "x")
+    M, C = x.shape
+    if out is None:
+        out = torch.empty((M, C), dtype=torch.float16, device=x.device)
+    op, ldy = _rows(out, "out")
+    st = lib.sdmoe_layernorm(xp, ldx, op, ldy, M, C, _dev(gamma, "gamma"), _dev(beta, "beta"), float(eps), _stream())
+    _lib.check(st, "sdmoe_layernorm")
+    return out
+
+
+def attention(q, k, v, nimg, Nq, Nk, heads, out=None, scale=None):
+    """softmax(q k^T * scale) v per (image, head); q [nimg*Nq, heads*d], k/v [nimg*Nk, heads*d] views."""
+    lib = _lib.load()
+    qp, ldq = _rows(q, "q")
+    kp, ldk = _rows(k, "k")
+    vp, ldv = _rows(v, "v")
+    C = q.shape[1]
+    d = C // heads
+    if out is None:
+        out = torch.empty((nimg * Nq, C), dtype=torch.float16, device=q.device)
+    op, ldo = _rows(out, "out")
+    if scale is None:
+        scale = d ** -0.5
+    st = lib.sdmoe_attention(qp, ldq, kp, ldk, vp, ldv, op, ldo, nimg, Nq, Nk, heads, d, float(scale), _stream())
+    _lib.check(st, "sdmoe_attention")
+    return out
+
+
+class Routing:
+    """Device-side expert layout of one MoE-fied GEGLU: labels [F] int32 and the per-expert neuron lists
+    (CSR), built once from the reference's `module.patterns` [E, F] (helper.py:48-62) or its label file."""
+
+    def __init__(self, labels: torch.Tensor, num_experts: int, k: int, device):
+        labels = labels.to(torch.int64).cpu()
+        F = labels.numel()
+        if labels.min() < 0 or labels.max() >= num_experts:
+            raise ValueError("expert labels out of range")
+        order = torch.argsort(labels, stable=True)
+        counts = torch.bincount(labels, minlength=num_experts)
+        off = torch.zeros(num_experts + 1, dtype=torch.int64)
+        off[1:] = torch.cumsum(counts, 0)
+        self.F, self.E, self.k = F, int(num_experts), int(k)
+        self.labels = labels.to(torch.int32).to(device)
+        self.e_off = off.to(torch.int32).to(device)
+        self.e_nid = order.to(torch.int32).to(device)
+
+    @classmethod
+    def from_patterns(cls, patterns: torch.Tensor, k: int, device=None):
+        p = patterns.detach().float().cpu()
+        E, F = p.shape
+        if not torch.all((p == 0) | (p == 1)) or not torch.all(p.sum(0) == 1):
+            raise ValueError("patterns must be a 0/1 [E, F] matrix with exactly one expert per neuron")
+        labels = p.argmax(0)
+        return cls(labels, E, k, device or patterns.device)
+
+
+def removed_bits(expert_ids, num_experts: int, device) -> torch.Tensor:
+    """uint32-packed (as int32) bitmask of removed experts."""
+    nw = (num_experts + 31) // 32
+    words = [0] * nw
+    for e in expert_ids:
+        e = int(e)
+        if not 0 <= e < num_experts:
+            raise IndexError(f"expert id {e} out of range [0, {num_experts})")
+        words[e >> 5] |= 1 << (e & 31)
+    words = [w - (1 << 32) if w >= (1 << 31) else w for w in words]
+    return torch.tensor(words, dtype=torch.int32, device=device)
+
+
+def geglu_route(y, routing: Routing | None, act=ACT_GELU, removed=None, out=None, gate_out=None, sel_out=None,
+                score_out=None):
+    """Routed GEGLU over y = proj(x) [M, 2F]; routing None -> dense value*act(gate)."""
+    lib = _lib.load()
+    yp, ldy = _rows(y, "y")
+    M = y.shape[0]
+    F = y.shape[1] // 2
+    if out is None:
+        out = torch.empty((M, F), dtype=torch.float16, device=y.device)
+    op, ldo = _rows(out, "out")
+    gp, ldg = (None, 0) if gate_out is None else _rows(gate_out, "gate_out")
+    if routing is None:
+        E, k, lab, off, nid = 0, 0, None, None, None
+    else:
+        if routing.F != F:
+            raise ValueError(f"routing has F={routing.F}, projection gives F={F}")
+        E, k = routing.E, routing.k
+        lab, off, nid = routing.labels.data_ptr(), routing.e_off.data_ptr(), routing.e_nid.data_ptr()
+    st = lib.sdmoe_geglu_route(yp, ldy, M, F, E, k, act, lab, off, nid, _ptr(removed), op, ldo, gp, ldg,
+                               _ptr(sel_out), _ptr(score_out), _stream())
+    _lib.check(st, "sdmoe_geglu_route")
+    return out
+
+
+def timestep_embedding(t: float, dim: int, device, flip_sin_to_cos=True, freq_shift=0.0, out=None, t_dev=None):
+    lib = _lib.load()
+    if out is None:
+        out = torch.empty((1, dim), dtype=torch.float16, device=device)
+    st = lib.sdmoe_timestep_embedding(out.data_ptr(), _ptr(t_dev), float(t), dim, int(flip_sin_to_cos),
+                                      float(freq_shift), _stream())
+    _lib.check(st, "sdmoe_timestep_embedding")
+    return out
+
+
+def prepare_input(lat: torch.Tensor, out: torch.Tensor, ncopy: int):
+    lib = _lib.load()
+    B, C, H, W = lat.shape
+    op, ldo = _rows(out, "out")
+    st = lib.sdmoe_prepare_input(_dev(lat, "lat", torch.float32), op, B, H * W, ldo, ncopy, _stream())
+    _lib.check(st, "sdmoe_prepare_input")
+    return out
+
+
+def cfg_ddim_step(eps: torch.Tensor, lat: torch.Tensor, do_cfg: bool, guidance: float, alpha_t: float,
+                  alpha_prev: float, next_in: torch.Tensor | None = None):
+    lib = _lib.load()
+    B, C, H, W = lat.shape
+    ep, lde = _rows(eps, "eps")
+    np_, ldn = (None, 0) if next_in is None else _rows(next_in, "next_in")
+    st = lib.sdmoe_cfg_ddim_step(ep, lde, _dev(lat, "lat", torch.float32), B, H * W, int(bool(do_cfg)),
+                                 float(guidance), float(alpha_t), float(alpha_prev), np_, ldn, _stream())
+    _lib.check(st, "sdmoe_cfg_ddim_step")
+    return lat
+
+
+def add(a, b, out=None):
+    lib = _lib.load()
+    if out is None:
+        out = torch.empty_like(a)
+    st = lib.sdmoe_add(_dev(a, "a"), _dev(b, "b"), _dev(out, "out"), a.numel(), _stream())
+    _lib.check(st, "sdmoe_add")
+    return out

@@ -1,0 +1,107 @@
+"""StableDiffusionPipeline stand-in: synthetic text conditioning + DDIM + classifier-free guidance, with the
+denoising loop entirely on the GPU (U-Net on the sdmoe kernels, CFG + DDIM update in one HIP kernel).
+
+Call shape kept from diffusers / the reference's callers: `pipe(prompt_or_list, safety_checker=...)` returns
+an object with `.images` (base_receiver.py:73, remove_wanda_neurons_fast.py:127-130, eval_coco.py:266-272).
+The CLIP text encoder and the VAE decoder are outside this tier: prompts map to seeded
+synthetic [77, 768] embeddings and `.images` holds the final latents ([4, H, W] fp32 per prompt).
+"""
+from __future__ import annotations
+
+import zlib
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import ops
+from .config import UNetConfig
+from .unet import CTX_LEN, IN_PAD, OUT_PAD, UNet2DConditionModel
+from .weights import make_state_dict
+
+
+def ddim_schedule(num_inference_steps=50, num_train_timesteps=1000, beta_start=0.00085, beta_end=0.012,
+                  steps_offset=1, set_alpha_to_one=False):
+    """DDIMScheduler as SD-1.x configures it (scaled_linear betas, 'leading' spacing, steps_offset=1):
+    returns (timesteps, alpha_cumprod[t], alpha_cumprod[prev t]) as host lists (scheduler constants)."""
+    betas = torch.linspace(beta_start ** 0.5, beta_end ** 0.5, num_train_timesteps, dtype=torch.float32) ** 2
+    ac = torch.cumprod(1.0 - betas, dim=0)
+    final = 1.0 if set_alpha_to_one else float(ac[0])
+    ratio = num_train_timesteps // num_inference_steps
+    ts = (np.arange(0, num_inference_steps) * ratio).round()[::-1].astype(np.int64) + steps_offset
+    a_t = [float(ac[t]) for t in ts]
+    a_prev = [float(ac[t - ratio]) if t - ratio >= 0 else final for t in ts]
+    return [int(t) for t in ts], a_t, a_prev
+
+
+def prompt_embedding(prompt: str, dim: int = 768) -> torch.Tensor:
+    """Seeded synthetic text conditioning [77, dim] fp32 (CPU) standing in for the CLIP text encoder."""
+    rng = np.random.default_rng(zlib.crc32(prompt.encode("utf-8")))
+    return torch.from_numpy((rng.standard_normal((CTX_LEN, dim)) * 0.5).astype(np.float32))
+
+
+def initial_latents(seed: int, index: int, cfg: UNetConfig) -> torch.Tensor:
+    """Per-prompt latents from a CPU generator seeded by (seed, global prompt index): identical for any
+    world size / sharding."""
+    g = torch.Generator().manual_seed(int(seed) * 1_000_003 + int(index))
+    return torch.randn((1, cfg.in_channels, cfg.sample_size, cfg.sample_size), generator=g)
+
+
+@dataclass
+class PipelineOutput:
+    images: list
+
+
+class StableDiffusionPipeline:
+    def __init__(self, unet: UNet2DConditionModel, device="cuda", num_inference_steps=50, guidance_scale=7.5):
+        self.unet = unet
+        self.config = unet.config
+        self.device = torch.device(device)
+        self.num_inference_steps = num_inference_steps
+        self.guidance_scale = guidance_scale
+        self.prompt_offset = 0  # global index of the first prompt (data-parallel shards set this per rank)
+
+    @classmethod
+    def synthetic(cls, cfg: UNetConfig | None = None, seed: int = 0, device="cuda", **kw):
+        cfg = cfg or UNetConfig.sd14()
+        unet = UNet2DConditionModel.from_state_dict(make_state_dict(cfg, seed), cfg, device)
+        return cls(unet, device, **kw)
+
+    def encode_prompt(self, prompts):
+        """[uncond x B ; cond x B] context rows [2B*77, dim] fp16 on device (uncond first, as diffusers)."""
+        dim = self.config.cross_attention_dim
+        embs = [prompt_embedding("", dim)] * len(prompts) + [prompt_embedding(p, dim) for p in prompts]
+        return torch.cat(embs, 0).to(self.device, torch.float16).contiguous()
+
+    def __call__(self, prompt, num_inference_steps=None, guidance_scale=None, latents=None, seed=None,
+                 prompt_offset=None, safety_checker=None, output_type="latent", **unused):
+        prompts = [prompt] if isinstance(prompt, str) else list(prompt)
+        B = len(prompts)
+        cfg = self.config
+        steps = num_inference_steps or self.num_inference_steps
+        g = self.guidance_scale if guidance_scale is None else guidance_scale
+        do_cfg = g > 1.0
+        if seed is None:
+            seed = torch.initial_seed()  # receivers call torch.manual_seed(self.seed) first (base_receiver.py:70)
+        if prompt_offset is None:
+            prompt_offset = self.prompt_offset
+        if latents is None:
+            latents = torch.cat([initial_latents(seed, prompt_offset + i, cfg) for i in range(B)])
+        lat = latents.to(self.device, torch.float32).contiguous()
+        ncopy = 2 if do_cfg else 1
+        ctx = self.encode_prompt(prompts)
+        if not do_cfg:
+            ctx = ctx[B * CTX_LEN:]
+        HW = cfg.sample_size * cfg.sample_size
+        x_in = torch.zeros((ncopy * B * HW, IN_PAD), dtype=torch.float16, device=self.device)
+        eps = torch.empty((ncopy * B * HW, OUT_PAD), dtype=torch.float16, device=self.device)
+        ops.prepare_input(lat, x_in, ncopy)
+        ts, a_t, a_prev = ddim_schedule(steps)
+        for s, t in enumerate(ts):
+            self.unet.forward_nhwc(x_in, float(t), ctx, out=eps)
+            ops.cfg_ddim_step(eps, lat, do_cfg, g, a_t[s], a_prev[s], next_in=x_in)
+        return PipelineOutput(images=[lat[i] for i in range(B)])
+
+    def to(self, device):
+        """Weights are placed at construction; kept for the reference's `model.to(args.gpu)` call shape."""
+        return self

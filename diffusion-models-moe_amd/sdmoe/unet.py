@@ -1,0 +1,481 @@
+"""SD-1.x UNet2DConditionModel on the sdmoe HIP kernels (gfx950), with diffusers' module tree and names.
+
+The module tree exists so the reference's receiver API works unchanged: `model.unet.named_modules()` yields
+`down_blocks.0.attentions.0.transformer_blocks.0.ff.net.0` (a GEGLU) and `...ff.net.2` (a
+LoRACompatibleLinear), forward hooks registered on them fire once per U-Net call in execution order, and
+`module.patterns` / `module.k` / `module.gelu` / `module.proj` mean what they mean in the reference
+(base_receiver.py:49-57, helper.py:48-62, relufy_model.py:28-40).
+
+Everything else is MI355X-first:
+  * activations live in HBM as NHWC fp16 [images*H*W, C] (the transformer's token layout, so no permutes);
+  * skip concatenations are zero-copy: each up-block ResNet input is one [rows, C_prev + C_skip] buffer; the
+    down path writes its skip outputs straight into the right-hand channel slice and reads them from there;
+  * GroupNorm(+SiLU) is applied inside the consuming conv/GEMM's operand load (stats pass only), the time
+    embedding add, bias, residual adds and activations are GEMM/conv epilogues;
+  * attention projections are fused (QKV [3C, C], cross KV [2C, 768]) and attention reads the heads in place;
+  * all 22 ResNet time-embedding projections run as ONE GEMM per step.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import ops
+from .config import UNetConfig
+
+CTX_LEN = 77
+IN_PAD = 64    # conv_in input channels padded 4 -> 64 (K-step of the implicit GEMM)
+OUT_PAD = 8    # conv_out output channels padded 4 -> 8 (16-B epilogue stores)
+
+
+def _buf(t):
+    return nn.Parameter(t, requires_grad=False)
+
+
+class LoRACompatibleLinear(nn.Module):
+    """nn.Linear stand-in (diffusers 0.27 LoRACompatibleLinear naming); weight [out, in] fp16."""
+
+    def __init__(self, weight, bias=None):
+        super().__init__()
+        self.weight = _buf(weight)
+        self.bias = None if bias is None else _buf(bias)
+        self._sdmoe_deferred = 0
+
+    @property
+    def in_features(self):
+        return self.weight.shape[1]
+
+    @property
+    def out_features(self):
+        return self.weight.shape[0]
+
+    def run(self, x2d, **kw):
+        return ops.linear(x2d, self.weight, self.bias, **kw)
+
+    def forward(self, x, scale=1.0):
+        if self._sdmoe_deferred and self._forward_hooks:
+            return None  # a sdmoe receiver hook computes this module's output (no double compute)
+        shp = x.shape
+        return self.run(x.reshape(-1, shp[-1])).view(*shp[:-1], self.out_features)
+
+
+class Conv2d(nn.Module):
+    """3x3 conv; weight stored [Cout, 3, 3, Cin] fp16 (K-contiguous implicit-GEMM layout)."""
+
+    def __init__(self, weight, bias, stride=1):
+        super().__init__()
+        self.weight = _buf(weight)
+        self.bias = _buf(bias)
+        self.stride = stride
+
+
+class Norm(nn.Module):
+    def __init__(self, weight, bias, eps, groups=None):
+        super().__init__()
+        self.weight = _buf(weight)
+        self.bias = _buf(bias)
+        self.eps = eps
+        self.groups = groups
+
+    def stats(self, x2d, nimg, HW):
+        return ops.groupnorm_stats(x2d, nimg, HW, self.weight, self.bias, self.eps, self.groups)
+
+
+def act_code(fn):
+    """Map a GEGLU `.gelu` callable to the kernel's activation code (diffusers gelu or the relufied ReLU)."""
+    from_name = getattr(fn, "_sdmoe_act", None)
+    if from_name is not None:
+        return ops.ACT_BY_NAME[from_name]
+    if fn is F.gelu or fn is torch.nn.functional.gelu:
+        return ops.ACT_GELU
+    if fn is F.relu or fn is torch.relu:
+        return ops.ACT_RELU
+    raise NotImplementedError(f"GEGLU activation {fn!r} has no HIP kernel (supported: gelu, relu)")
+
+
+def _gelu(x):
+    return F.gelu(x)
+
+
+_gelu._sdmoe_act = "gelu"
+
+
+class GEGLU(nn.Module):
+    """diffusers GEGLU: proj = Linear(C, 8C); out = value * gelu(gate) (value = first half).
+
+    MoE-fication state (set by moefication.helper.modify_ffn): `patterns` [E, 4C] 0/1 and `k`."""
+
+    def __init__(self, proj: LoRACompatibleLinear):
+        super().__init__()
+        self.proj = proj
+        self.gelu = _gelu
+        self.patterns = None
+        self.k = None
+        self.bounding_box = None
+        self._routing = None
+        self._routing_key = None
+        self._sdmoe_deferred = 0
+
+    @property
+    def inner_dim(self):
+        return self.proj.out_features // 2
+
+    def routing(self):
+        """Device expert layout for the current (patterns, k); rebuilt only when either changes."""
+        if self.patterns is None:
+            return None
+        key = (id(self.patterns), self.patterns.data_ptr(), int(self.k))
+        if self._routing_key != key:
+            if getattr(self, "labels", None) is not None and self.labels.numel() == self.inner_dim:
+                self._routing = ops.Routing(self.labels, self.patterns.shape[0], int(self.k), self.proj.weight.device)
+            else:
+                self._routing = ops.Routing.from_patterns(self.patterns, int(self.k), self.proj.weight.device)
+            self._routing_key = key
+        return self._routing
+
+    def routed(self, x, removed=None, want_gate=False):
+        """proj GEMM + routed GEGLU kernel. x: [..., C] fp16. Returns (out [..., 4C], masked gate or None)."""
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1])
+        y = self.proj.run(x2)
+        gate = torch.empty((x2.shape[0], self.inner_dim), dtype=torch.float16, device=x.device) if want_gate else None
+        out = ops.geglu_route(y, self.routing(), act_code(self.gelu), removed=removed, gate_out=gate)
+        out = out.view(*shp[:-1], self.inner_dim)
+        return out, (gate.view(*shp[:-1], self.inner_dim) if want_gate else None)
+
+    def forward(self, x, scale=1.0):
+        if self._sdmoe_deferred and self._forward_hooks:
+            return None  # a sdmoe receiver hook computes the routed output (no double compute)
+        return self.routed(x)[0]
+
+
+class FeedForward(nn.Module):
+    def __init__(self, geglu, down):
+        super().__init__()
+        self.net = nn.ModuleList([geglu, nn.Dropout(0.0), down])
+
+    def run(self, x2d, nimg, residual):
+        geglu, down = self.net[0], self.net[2]
+        h = geglu(x2d.view(nimg, -1, x2d.shape[1]))
+        if down._forward_hooks:
+            o = down(h)
+            return ops.add(o.reshape(residual.shape).contiguous(), residual)
+        return down.run(h.reshape(-1, h.shape[-1]), residual=residual)
+
+
+class Attention(nn.Module):
+    def __init__(self, wq, wk, wv, wo, bo, heads, self_attn):
+        super().__init__()
+        self.heads = heads
+        self.self_attn = self_attn
+        C = wq.shape[0]
+        if self_attn:
+            self.w_qkv = _buf(torch.cat([wq, wk, wv], 0).contiguous())
+            self.to_q = LoRACompatibleLinear(self.w_qkv.data[:C])
+            self.to_k = LoRACompatibleLinear(self.w_qkv.data[C:2 * C])
+            self.to_v = LoRACompatibleLinear(self.w_qkv.data[2 * C:])
+        else:
+            self.w_kv = _buf(torch.cat([wk, wv], 0).contiguous())
+            self.to_q = LoRACompatibleLinear(wq)
+            self.to_k = LoRACompatibleLinear(self.w_kv.data[:C])
+            self.to_v = LoRACompatibleLinear(self.w_kv.data[C:])
+        self.to_out = nn.ModuleList([LoRACompatibleLinear(wo, bo), nn.Dropout(0.0)])
+
+    def run(self, x2d, nimg, N, residual, ctx2d=None):
+        C = x2d.shape[1]
+        if self.self_attn:
+            qkv = ops.linear(x2d, self.w_qkv)
+            a = ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], nimg, N, N, self.heads)
+        else:
+            q = ops.linear(x2d, self.to_q.weight)
+            kv = ops.linear(ctx2d, self.w_kv)
+            a = ops.attention(q, kv[:, :C], kv[:, C:], nimg, N, ctx2d.shape[0] // nimg, self.heads)
+        return self.to_out[0].run(a, residual=residual)
+
+
+class BasicTransformerBlock(nn.Module):
+    def __init__(self, norm1, attn1, norm2, attn2, norm3, ff):
+        super().__init__()
+        self.norm1, self.attn1, self.norm2, self.attn2, self.norm3, self.ff = norm1, attn1, norm2, attn2, norm3, ff
+
+    def run(self, hs, nimg, N, ctx2d):
+        n = ops.layernorm(hs, self.norm1.weight, self.norm1.bias, self.norm1.eps)
+        hs = self.attn1.run(n, nimg, N, residual=hs)
+        n = ops.layernorm(hs, self.norm2.weight, self.norm2.bias, self.norm2.eps)
+        hs = self.attn2.run(n, nimg, N, residual=hs, ctx2d=ctx2d)
+        n = ops.layernorm(hs, self.norm3.weight, self.norm3.bias, self.norm3.eps)
+        return self.ff.run(n, nimg, residual=hs)
+
+
+class Transformer2DModel(nn.Module):
+    def __init__(self, norm, proj_in, block, proj_out):
+        super().__init__()
+        self.norm = norm
+        self.proj_in = proj_in
+        self.transformer_blocks = nn.ModuleList([block])
+        self.proj_out = proj_out
+
+    def run(self, x, nimg, HW, ctx2d, out):
+        sc, sh = self.norm.stats(x, nimg, HW)
+        hs = self.proj_in.run(x, gn=(sc, sh, False), rows_per_batch=HW)
+        hs = self.transformer_blocks[0].run(hs, nimg, HW, ctx2d)
+        return self.proj_out.run(hs, residual=x, out=out)
+
+
+class ResnetBlock2D(nn.Module):
+    def __init__(self, norm1, conv1, temb_proj, norm2, conv2, shortcut):
+        super().__init__()
+        self.norm1, self.conv1, self.time_emb_proj, self.norm2, self.conv2 = norm1, conv1, temb_proj, norm2, conv2
+        self.conv_shortcut = shortcut
+        self.temb_slice = None  # (offset, Cout) into the fused time-embedding projection output
+
+    def run(self, x, nimg, H, W, temb_all, out):
+        HW = H * W
+        sc1, sh1 = self.norm1.stats(x, nimg, HW)
+        o, n = self.temb_slice
+        h = ops.conv3x3(x, nimg, H, W, self.conv1.weight, self.conv1.bias, gn=(sc1, sh1, True),
+                        coladd=temb_all[:, o:o + n], coladd_bstride=0)
+        sc2, sh2 = self.norm2.stats(h, nimg, HW)
+        res = x if self.conv_shortcut is None else self.conv_shortcut.run(x)
+        return ops.conv3x3(h, nimg, H, W, self.conv2.weight, self.conv2.bias, gn=(sc2, sh2, True), residual=res,
+                           out=out)
+
+
+class Sampler(nn.Module):
+    def __init__(self, conv):
+        super().__init__()
+        self.conv = conv
+
+
+class Block(nn.Module):
+    """Down/mid/up block container with diffusers' child names (resnets / attentions / down|upsamplers)."""
+
+    def __init__(self, resnets, attentions=None, downsamplers=None, upsamplers=None):
+        super().__init__()
+        self.resnets = nn.ModuleList(resnets)
+        if attentions:
+            self.attentions = nn.ModuleList(attentions)
+        else:
+            self.attentions = None
+        if downsamplers:
+            self.downsamplers = nn.ModuleList(downsamplers)
+        if upsamplers:
+            self.upsamplers = nn.ModuleList(upsamplers)
+
+
+class TimestepEmbedding(nn.Module):
+    def __init__(self, l1, l2):
+        super().__init__()
+        self.linear_1, self.linear_2 = l1, l2
+
+
+class UNet2DConditionModel(nn.Module):
+    def __init__(self, cfg: UNetConfig):
+        super().__init__()
+        self.config = cfg
+
+    # ------------------------------------------------------------------ construction
+    @classmethod
+    def from_state_dict(cls, sd, cfg: UNetConfig, device="cuda"):
+        """Build from a diffusers-layout state dict (fp32/fp16 CPU tensors), converting layouts once."""
+        m = cls(cfg)
+        dev = torch.device(device)
+
+        def t(name):
+            return sd[name].to(dev, torch.float16).contiguous()
+
+        def lin(p, bias=True):
+            return LoRACompatibleLinear(t(p + ".weight"), t(p + ".bias") if bias else None)
+
+        def conv(p, stride=1):
+            w = sd[p + ".weight"].to(dev, torch.float16).permute(0, 2, 3, 1).contiguous()
+            return Conv2d(w, t(p + ".bias"), stride)
+
+        def conv1x1(p):
+            w = sd[p + ".weight"]
+            return LoRACompatibleLinear(w.reshape(w.shape[0], w.shape[1]).to(dev, torch.float16).contiguous(),
+                                        t(p + ".bias"))
+
+        def gn(p, eps):
+            return Norm(t(p + ".weight"), t(p + ".bias"), eps, cfg.norm_num_groups)
+
+        def ln(p):
+            return Norm(t(p + ".weight"), t(p + ".bias"), cfg.layer_norm_eps)
+
+        def resnet(p):
+            sc = conv1x1(p + ".conv_shortcut") if (p + ".conv_shortcut.weight") in sd else None
+            return ResnetBlock2D(gn(p + ".norm1", cfg.norm_eps), conv(p + ".conv1"), lin(p + ".time_emb_proj"),
+                                 gn(p + ".norm2", cfg.norm_eps), conv(p + ".conv2"), sc)
+
+        def transformer(p):
+            b = p + ".transformer_blocks.0"
+            a1 = Attention(t(b + ".attn1.to_q.weight"), t(b + ".attn1.to_k.weight"), t(b + ".attn1.to_v.weight"),
+                           t(b + ".attn1.to_out.0.weight"), t(b + ".attn1.to_out.0.bias"), cfg.attention_heads, True)
+            a2 = Attention(t(b + ".attn2.to_q.weight"), t(b + ".attn2.to_k.weight"), t(b + ".attn2.to_v.weight"),
+                           t(b + ".attn2.to_out.0.weight"), t(b + ".attn2.to_out.0.bias"), cfg.attention_heads, False)
+            ff = FeedForward(GEGLU(lin(b + ".ff.net.0.proj")), lin(b + ".ff.net.2"))
+            blk = BasicTransformerBlock(ln(b + ".norm1"), a1, ln(b + ".norm2"), a2, ln(b + ".norm3"), ff)
+            return Transformer2DModel(gn(p + ".norm", cfg.transformer_norm_eps), conv1x1(p + ".proj_in"), blk,
+                                      conv1x1(p + ".proj_out"))
+
+        w_in = sd["conv_in.weight"].to(dev, torch.float16)
+        w_in = F.pad(w_in, (0, 0, 0, 0, 0, IN_PAD - w_in.shape[1])).permute(0, 2, 3, 1).contiguous()
+        m.conv_in = Conv2d(w_in, t("conv_in.bias"))
+        m.time_embedding = TimestepEmbedding(lin("time_embedding.linear_1"), lin("time_embedding.linear_2"))
+        nblk = len(cfg.block_out_channels)
+        L = cfg.layers_per_block
+        downs = []
+        for i, typ in enumerate(cfg.down_block_types):
+            res = [resnet(f"down_blocks.{i}.resnets.{j}") for j in range(L)]
+            att = [transformer(f"down_blocks.{i}.attentions.{j}") for j in range(L)] if typ.startswith("CrossAttn") \
+                else None
+            ds = [Sampler(conv(f"down_blocks.{i}.downsamplers.0.conv", 2))] if i < nblk - 1 else None
+            downs.append(Block(res, att, downsamplers=ds))
+        m.down_blocks = nn.ModuleList(downs)
+        m.mid_block = Block([resnet("mid_block.resnets.0"), resnet("mid_block.resnets.1")],
+                            [transformer("mid_block.attentions.0")])
+        ups = []
+        for i, typ in enumerate(cfg.up_block_types):
+            res = [resnet(f"up_blocks.{i}.resnets.{j}") for j in range(L + 1)]
+            att = [transformer(f"up_blocks.{i}.attentions.{j}") for j in range(L + 1)] \
+                if typ.startswith("CrossAttn") else None
+            us = [Sampler(conv(f"up_blocks.{i}.upsamplers.0.conv"))] if i < nblk - 1 else None
+            ups.append(Block(res, att, upsamplers=us))
+        m.up_blocks = nn.ModuleList(ups)
+        m.conv_norm_out = gn("conv_norm_out", cfg.norm_eps)
+        w_out = sd["conv_out.weight"].to(dev, torch.float16)
+        w_out = F.pad(w_out, (0, 0, 0, 0, 0, 0, 0, OUT_PAD - w_out.shape[0])).permute(0, 2, 3, 1).contiguous()
+        b_out = F.pad(sd["conv_out.bias"].to(dev, torch.float16), (0, OUT_PAD - cfg.out_channels)).contiguous()
+        m.conv_out = Conv2d(w_out, b_out)
+
+        # fuse every ResNet's time_emb_proj into one [sum Cout, temb] GEMM; modules keep views
+        resnets = [r for _, r in m.named_modules() if isinstance(r, ResnetBlock2D)]
+        ws = torch.cat([r.time_emb_proj.weight.data for r in resnets], 0).contiguous()
+        bs = torch.cat([r.time_emb_proj.bias.data for r in resnets], 0).contiguous()
+        m.temb_w, m.temb_b = _buf(ws), _buf(bs)
+        off = 0
+        for r in resnets:
+            n = r.time_emb_proj.weight.shape[0]
+            r.time_emb_proj.weight = _buf(ws[off:off + n])
+            r.time_emb_proj.bias = _buf(bs[off:off + n])
+            r.temb_slice = (off, n)
+            off += n
+        return m
+
+    # ------------------------------------------------------------------ forward
+    def time_embed(self, t, t_dev=None):
+        cfg = self.config
+        dev = self.conv_in.weight.device
+        e = ops.timestep_embedding(t, cfg.block_out_channels[0], dev, cfg.flip_sin_to_cos, cfg.freq_shift, t_dev=t_dev)
+        e = self.time_embedding.linear_1.run(e, act=ops.ACT_SILU)
+        e = self.time_embedding.linear_2.run(e, act=ops.ACT_SILU)  # every consumer applies SiLU(temb) first
+        return ops.linear(e, self.temb_w, self.temb_b)
+
+    def forward_nhwc(self, x_in, t, ctx2d, out=None, t_dev=None):
+        """One U-Net evaluation. x_in: [nimg*H*W, 64] fp16 (channels 0..3 = latent), ctx2d: [nimg*77, 768].
+        Returns eps as [nimg*H*W, 8] fp16 (channels 0..3 valid)."""
+        cfg = self.config
+        dev = x_in.device
+        nimg = ctx2d.shape[0] // CTX_LEN
+        H = W = cfg.sample_size
+        ch = cfg.block_out_channels
+        nblk = len(ch)
+        L = cfg.layers_per_block
+        temb_all = self.time_embed(t, t_dev)
+
+        # ---- plan the up-path concat buffers [rows, C_prev + C_skip] (consumption order)
+        rev = list(reversed(ch))
+        sizes = [H >> i for i in range(nblk)]
+        up_in = []
+        prev = rev[0]
+        for i in range(nblk):
+            cout = rev[i]
+            skip_in = rev[min(i + 1, nblk - 1)]
+            hh = sizes[nblk - 1 - i]
+            for j in range(L + 1):
+                cp = prev if j == 0 else cout
+                cs = skip_in if j == L else cout
+                buf = torch.empty((nimg * hh * hh, cp + cs), dtype=torch.float16, device=dev)
+                up_in.append((buf, cp, hh))
+            prev = cout
+        nskip = len(up_in)
+
+        def skip_slot(k):  # k-th produced skip -> right-hand slice of its consumer's concat buffer
+            buf, cp, _ = up_in[nskip - 1 - k]
+            return buf[:, cp:]
+
+        def new(rows, c):
+            return torch.empty((rows, c), dtype=torch.float16, device=dev)
+
+        # ---- down path
+        k = 0
+        h = ops.conv3x3(x_in, nimg, H, W, self.conv_in.weight, self.conv_in.bias, out=skip_slot(k))
+        k += 1
+        hh = H
+        for i, blk in enumerate(self.down_blocks):
+            rows = nimg * hh * hh
+            for j in range(L):
+                if blk.attentions is not None:
+                    r = blk.resnets[j].run(h, nimg, hh, hh, temb_all, out=new(rows, ch[i]))
+                    h = blk.attentions[j].run(r, nimg, hh * hh, ctx2d, out=skip_slot(k))
+                else:
+                    h = blk.resnets[j].run(h, nimg, hh, hh, temb_all, out=skip_slot(k))
+                k += 1
+            if hasattr(blk, "downsamplers"):
+                c = blk.downsamplers[0].conv
+                h = ops.conv3x3(h, nimg, hh, hh, c.weight, c.bias, stride=2, out=skip_slot(k))
+                k += 1
+                hh //= 2
+
+        # ---- mid
+        rows = nimg * hh * hh
+        mb = self.mid_block
+        r = mb.resnets[0].run(h, nimg, hh, hh, temb_all, out=new(rows, ch[-1]))
+        a = mb.attentions[0].run(r, nimg, hh * hh, ctx2d, out=new(rows, ch[-1]))
+        buf0, cp0, _ = up_in[0]
+        mb.resnets[1].run(a, nimg, hh, hh, temb_all, out=buf0[:, :cp0])
+
+        # ---- up path
+        idx = 0
+        final = None
+        for i, blk in enumerate(self.up_blocks):
+            cout = rev[i]
+            for j in range(L + 1):
+                inp, cp, hh = up_in[idx]
+                rows = nimg * hh * hh
+                last_in_block = j == L
+                has_up = hasattr(blk, "upsamplers")
+                if not last_in_block:
+                    nb, ncp, _ = up_in[idx + 1]
+                    dest = nb[:, :ncp]
+                elif has_up or i == nblk - 1:
+                    dest = new(rows, cout)
+                if blk.attentions is not None:
+                    r = blk.resnets[j].run(inp, nimg, hh, hh, temb_all, out=new(rows, cout))
+                    o = blk.attentions[j].run(r, nimg, hh * hh, ctx2d, out=dest)
+                else:
+                    o = blk.resnets[j].run(inp, nimg, hh, hh, temb_all, out=dest)
+                idx += 1
+                if last_in_block:
+                    if has_up:
+                        nb, ncp, _ = up_in[idx]
+                        c = blk.upsamplers[0].conv
+                        ops.conv3x3(o, nimg, hh, hh, c.weight, c.bias, upsample=True, out=nb[:, :ncp])
+                    else:
+                        final = o
+
+        # ---- out
+        sc, sh = self.conv_norm_out.stats(final, nimg, H * W)
+        if out is None:
+            out = new(nimg * H * W, OUT_PAD)
+        return ops.conv3x3(final, nimg, H, W, self.conv_out.weight, self.conv_out.bias, gn=(sc, sh, True), out=out)
+
+    def forward(self, sample, timestep, encoder_hidden_states):
+        """diffusers-style call: sample [n, 4, H, W], encoder_hidden_states [n, 77, ctx]; returns eps [n,4,H,W]."""
+        n, c, H, W = sample.shape
+        x = torch.zeros((n * H * W, IN_PAD), dtype=torch.float16, device=sample.device)
+        x[:, :c] = sample.permute(0, 2, 3, 1).reshape(n * H * W, c).to(torch.float16)
+        ctx = encoder_hidden_states.reshape(-1, encoder_hidden_states.shape[-1]).to(torch.float16).contiguous()
+        eps = self.forward_nhwc(x, float(timestep), ctx)
+        return eps[:, :c].reshape(n, H, W, c).permute(0, 3, 1, 2).contiguous()

@@ -1,0 +1,122 @@
+/*
+ * sdmoe.h — C ABI of libsdmoe_hip.so, the MI355X (gfx950) kernels behind the MoE-fied Stable-Diffusion
+ * denoising step of ruchikachavhan/diffusion-models-moe.
+ *
+ * Conventions (every entry point):
+ *   - plain device pointers (fp16 = IEEE binary16, fp32, int32) and sizes; no framework types;
+ *   - activations are row-major [rows, channels] with an explicit row stride `ld*` in ELEMENTS, so a
+ *     channel slice of a wider buffer (zero-copy skip concatenation, fused QKV) is passed as (ptr, ld);
+ *     spatial tensors are NHWC, i.e. [images * H * W, C];
+ *   - `stream` is a hipStream_t (pass torch.cuda.current_stream().cuda_stream); every call is asynchronous,
+ *     allocates nothing, never synchronises and is safe under hipGraph stream capture;
+ *   - return 0 on success, >0 a hipError_t from the launch, <0 an argument error:
+ *     -1 bad pointer/size, -2 unsupported shape/alignment, -3 unsupported mode.
+ *   The library neither frees nor retains caller buffers.
+ */
+#ifndef SDMOE_H
+#define SDMOE_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Activation codes for `act` arguments. */
+#define SDMOE_ACT_NONE 0
+#define SDMOE_ACT_SILU 1
+#define SDMOE_ACT_GELU 2 /* exact erf GELU, diffusers GEGLU.gelu / F.gelu */
+#define SDMOE_ACT_RELU 3 /* relufied U-Net, sparsity/relufy_model.py:8-15 */
+
+const char* sdmoe_version(void);
+
+/*
+ * C[m, n] = act( sum_k A'[m, k] * W[n, k] + bias[n] + coladd[m / rows_per_batch][n] ) + R[m, n]
+ * A' = A, or GroupNorm-applied A: A[m,k]*a_scale[img,k] + a_shift[img,k] (img = m / rows_per_batch), SiLU'd
+ * when a_silu.  W is nn.Linear layout [N, K]; wmask_bits (optional) is a bitmask [N][K/8] bytes, bit j of byte
+ * (n*K + k)/8 set => W[n, k] treated as 0.
+ * Replaces: torch.nn.Linear / LoRACompatibleLinear.forward on the U-Net hot path (diffusers, external), the
+ * GEGLU projection recomputed by MOEFy.hook_fn (neuron_receivers/moefy.py:12) and RemoveExperts.hook_fn
+ * (neuron_receivers/remove_skilled_experts.py:26), and the masked down-projection
+ * F.linear(x, W*(1-M), b) of WandaRemoveNeuronsFast.linear_hook_fn (neuron_receivers/remove_wanda_neurons_fast.py:69-83).
+ * Requires K % 64 == 0, N % 8 == 0, strides % 8 == 0.
+ */
+int sdmoe_linear(const void* A, long lda, const void* W, long ldw, const void* bias, const void* coladd,
+                 long coladd_bstride, int rows_per_batch, const void* R, long ldr, void* C, long ldc, int M, int N,
+                 int K, int act, const float* a_scale, const float* a_shift, int a_silu, const void* wmask_bits,
+                 void* stream);
+
+/*
+ * 3x3 convolution, padding 1, on NHWC X [nimg, H, W, Cin] (pixel stride ldx): stride 1 or 2, or a fused
+ * nearest-neighbour 2x upsample in front (upsample=1, output 2H x 2W). Weights [Cout][3][3][Cin].
+ * Same optional fusions as sdmoe_linear (GroupNorm+SiLU on the input, bias, per-image coladd (time
+ * embedding), activation, residual R).
+ * Replaces: diffusers ResnetBlock2D conv1/conv2 (+norm/SiLU/temb add/residual), Downsample2D, Upsample2D,
+ * conv_in/conv_out of UNet2DConditionModel (external). Requires Cin % 64 == 0, Cout % 8 == 0.
+ */
+int sdmoe_conv3x3(const void* X, long ldx, int nimg, int H, int W, int Cin, const void* Wt, const void* bias,
+                  const void* coladd, long coladd_bstride, const void* R, long ldr, void* Y, long ldy, int Cout,
+                  int stride, int upsample, int act, const float* a_scale, const float* a_shift, int a_silu,
+                  void* stream);
+
+/*
+ * GroupNorm statistics of X [nimg, HW, C] (row stride ldx) with `groups` groups: writes per (image, channel)
+ * scale = rstd*gamma and shift = beta - mean*scale (fp32 [nimg, C]) consumed by the fused A-load above.
+ * workspace: >= nimg*groups*64*2 floats.
+ * Replaces: torch.nn.GroupNorm in ResnetBlock2D / Transformer2DModel / conv_norm_out (external).
+ */
+int sdmoe_groupnorm_stats(const void* X, long ldx, int nimg, int HW, int C, int groups, const void* gamma,
+                          const void* beta, float eps, float* scale, float* shift, float* workspace,
+                          long workspace_floats, void* stream);
+
+/* LayerNorm over the last dimension (C % 8 == 0, C <= 2048). Replaces BasicTransformerBlock norm1/2/3. */
+int sdmoe_layernorm(const void* X, long ldx, void* Y, long ldy, int M, int C, const void* gamma, const void* beta,
+                    float eps, void* stream);
+
+/*
+ * Scaled-dot-product attention, fp16: O[b, q, h*d:(h+1)*d] = softmax(Q K^T * scale) V per (image b, head h),
+ * with Q [nimg*Nq, *] (stride ldq), K/V [nimg*Nk, *] (strides ldk/ldv), head h at column offset h*head_dim.
+ * head_dim in {32, 40, 64, 80, 160}.
+ * Replaces: diffusers Attention (attn1 self / attn2 cross) + AttnProcessor softmax(QK^T/sqrt(d))V (external;
+ * SURVEY §2.3 K10).
+ */
+int sdmoe_attention(const void* Q, long ldq, const void* K, long ldk, const void* V, long ldv, void* O, long ldo,
+                    int nimg, int Nq, int Nk, int heads, int head_dim, float scale, void* stream);
+
+/*
+ * MoE-fied GEGLU routing over Y = proj(x) [M, 2F] (value | gate halves, row stride ldy), F = 4C inner neurons:
+ *   g = act(gate); score[e] = sum_{n: labels[n]==e} g[n]; removed experts score 0; sel = top-k(score) with
+ *   ties toward the lowest expert id; keep[n] = sel[labels[n]] && !removed[labels[n]];
+ *   out[m, n] = keep ? value*g : 0.
+ * labels [F] int32 (0..E-1); e_off [E+1] / e_nid [F]: neurons grouped per expert (ascending neuron id);
+ * removed_bits [ceil(E/32)] (bit e => expert e removed) or NULL; E == 0 => dense GEGLU (value * act(gate)).
+ * Optional outputs: gate_out [M, F] (the masked gate the reference appends to self.gates), sel_out
+ * [M, ceil(E/32)] uint32 top-k bitmask, score_out [M, E] fp16 scores. E <= 256, F % 8 == 0.
+ * Replaces: MOEFy.hook_fn (neuron_receivers/moefy.py:10-27) and RemoveExperts.hook_fn
+ * (neuron_receivers/remove_skilled_experts.py:24-55) after the projection: gelu, matmul(gate, patterns^T),
+ * torch.topk, F.embedding(...).sum(-2), gate[mask==0]=0, hidden_states*gate, gate.cpu().
+ */
+int sdmoe_geglu_route(const void* Y, long ldy, int M, int F, int E, int k, int act, const int* labels,
+                      const int* e_off, const int* e_nid, const unsigned* removed_bits, void* out, long ldo,
+                      void* gate_out, long ldg, unsigned* sel_out, void* score_out, void* stream);
+
+/* diffusers get_timestep_embedding for one timestep (t_dev if non-NULL, else t), fp16 [dim]. */
+int sdmoe_timestep_embedding(void* out, const float* t_dev, float t, int dim, int flip_sin_to_cos, float freq_shift,
+                             void* stream);
+
+/* latents fp32 NCHW [B,4,H,W] -> U-Net input fp16 NHWC [ncopy*B, HW, ldo] channels 0..3 (CFG copies). */
+int sdmoe_prepare_input(const float* lat, void* out, int B, int HW, long ldo, int ncopy, void* stream);
+
+/*
+ * Classifier-free guidance + DDIM (eta = 0) update of fp32 NCHW latents in place from eps fp16
+ * [ncopy*B, HW, lde] (uncond first); optionally writes the next fp16 U-Net input (both CFG copies).
+ * Replaces StableDiffusionPipeline's CFG combine + DDIMScheduler.step (external).
+ */
+int sdmoe_cfg_ddim_step(const void* eps, long lde, float* lat, int B, int HW, int do_cfg, float guidance,
+                        float alpha_t, float alpha_prev, void* next_in, long ldn, void* stream);
+
+/* out = a + b (fp16, n % 8 == 0). */
+int sdmoe_add(const void* a, const void* b, void* out, long n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SDMOE_H */

@@ -1,0 +1,169 @@
+"""ORACLE (test infrastructure only) — fp32 CPU restatement of the diffusers SD-1.x UNet2DConditionModel
+forward, DDIM scheduler and classifier-free-guidance loop that the reference's hooks run inside
+(utils.py:64-84 builds it; base_receiver.py:73 runs it). diffusers is not vendored in the reference and is
+absent here, so this U-Net body is PARITY-UNPINNED against diffusers itself: it restates diffusers 0.27's
+published module semantics (ResnetBlock2D, Transformer2DModel/BasicTransformerBlock, Attention, GEGLU,
+Downsample2D/Upsample2D, get_timestep_embedding, DDIMScheduler) and is checked by unit identities in
+tests/test_oracle_unet.py. The hook points reproduce where the reference's receivers attach:
+  ff_hook(layer, x, proj_w, proj_b)  <- forward hook on every `ff.net.0` GEGLU (base_receiver.py:49-53)
+  down_hook(layer, x, w, b)          <- forward hook on every `ff.net.2` Linear (remove_wanda_neurons_fast.py:107-112)
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline may import this module.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+
+def timestep_embedding(t, dim, flip_sin_to_cos=True, freq_shift=0.0, max_period=10000):
+    """diffusers.models.embeddings.get_timestep_embedding."""
+    half = dim // 2
+    exponent = -math.log(max_period) * torch.arange(half, dtype=torch.float32) / (half - freq_shift)
+    emb = torch.tensor([float(t)], dtype=torch.float32)[:, None] * torch.exp(exponent)[None, :]
+    emb = torch.cat([torch.sin(emb), torch.cos(emb)], dim=-1)
+    if flip_sin_to_cos:
+        emb = torch.cat([emb[:, half:], emb[:, :half]], dim=-1)
+    return emb
+
+
+class UNetRef:
+    def __init__(self, sd, cfg):
+        self.sd = {k: v.float() for k, v in sd.items()}
+        self.cfg = cfg
+        self.layer = 0
+
+    # -- primitives
+    def lin(self, x, name, bias=True):
+        return F.linear(x, self.sd[name + ".weight"], self.sd.get(name + ".bias") if bias else None)
+
+    def conv(self, x, name, stride=1, padding=1):
+        return F.conv2d(x, self.sd[name + ".weight"], self.sd[name + ".bias"], stride=stride, padding=padding)
+
+    def gn(self, x, name, eps):
+        return F.group_norm(x, self.cfg.norm_num_groups, self.sd[name + ".weight"], self.sd[name + ".bias"], eps)
+
+    def ln(self, x, name):
+        return F.layer_norm(x, (x.shape[-1],), self.sd[name + ".weight"], self.sd[name + ".bias"],
+                            self.cfg.layer_norm_eps)
+
+    # -- blocks
+    def resnet(self, x, temb, p):
+        h = F.silu(self.gn(x, p + ".norm1", self.cfg.norm_eps))
+        h = self.conv(h, p + ".conv1")
+        h = h + self.lin(F.silu(temb), p + ".time_emb_proj")[:, :, None, None]
+        h = F.silu(self.gn(h, p + ".norm2", self.cfg.norm_eps))
+        h = self.conv(h, p + ".conv2")
+        sc = self.conv(x, p + ".conv_shortcut", padding=0) if (p + ".conv_shortcut.weight") in self.sd else x
+        return sc + h
+
+    def attention(self, x, ctx, p):
+        heads = self.cfg.attention_heads
+        q = self.lin(x, p + ".to_q", bias=False)
+        src = x if ctx is None else ctx
+        k = self.lin(src, p + ".to_k", bias=False)
+        v = self.lin(src, p + ".to_v", bias=False)
+        B, N, C = q.shape
+        d = C // heads
+        q = q.view(B, N, heads, d).transpose(1, 2)
+        k = k.view(B, -1, heads, d).transpose(1, 2)
+        v = v.view(B, -1, heads, d).transpose(1, 2)
+        o = F.scaled_dot_product_attention(q, k, v)
+        o = o.transpose(1, 2).reshape(B, N, C)
+        return self.lin(o, p + ".to_out.0")
+
+    def feedforward(self, x, p):
+        layer = self.layer
+        self.layer += 1
+        w0, b0 = self.sd[p + ".net.0.proj.weight"], self.sd[p + ".net.0.proj.bias"]
+        if self.ff_hook is not None:
+            h = self.ff_hook(layer, x, w0, b0)
+        else:
+            hv, g = F.linear(x, w0, b0).chunk(2, dim=-1)
+            h = hv * F.gelu(g)
+        w2, b2 = self.sd[p + ".net.2.weight"], self.sd[p + ".net.2.bias"]
+        if self.down_hook is not None:
+            return self.down_hook(layer, h, w2, b2)
+        return F.linear(h, w2, b2)
+
+    def transformer(self, x, ctx, p):
+        B, C, H, W = x.shape
+        res = x
+        h = self.gn(x, p + ".norm", self.cfg.transformer_norm_eps)
+        h = self.conv(h, p + ".proj_in", padding=0)
+        h = h.permute(0, 2, 3, 1).reshape(B, H * W, C)
+        b = p + ".transformer_blocks.0"
+        h = self.attention(self.ln(h, b + ".norm1"), None, b + ".attn1") + h
+        h = self.attention(self.ln(h, b + ".norm2"), ctx, b + ".attn2") + h
+        h = self.feedforward(self.ln(h, b + ".norm3"), b + ".ff") + h
+        h = h.reshape(B, H, W, C).permute(0, 3, 1, 2)
+        return self.conv(h, p + ".proj_out", padding=0) + res
+
+    def __call__(self, sample, t, ctx, ff_hook=None, down_hook=None):
+        cfg = self.cfg
+        self.ff_hook, self.down_hook, self.layer = ff_hook, down_hook, 0
+        temb = timestep_embedding(t, cfg.block_out_channels[0], cfg.flip_sin_to_cos, cfg.freq_shift)
+        temb = self.lin(F.silu(self.lin(temb, "time_embedding.linear_1")), "time_embedding.linear_2")
+        h = self.conv(sample, "conv_in")
+        skips = [h]
+        L = cfg.layers_per_block
+        nblk = len(cfg.block_out_channels)
+        for i, typ in enumerate(cfg.down_block_types):
+            for j in range(L):
+                h = self.resnet(h, temb, f"down_blocks.{i}.resnets.{j}")
+                if typ.startswith("CrossAttn"):
+                    h = self.transformer(h, ctx, f"down_blocks.{i}.attentions.{j}")
+                skips.append(h)
+            if i < nblk - 1:
+                h = self.conv(h, f"down_blocks.{i}.downsamplers.0.conv", stride=2)
+                skips.append(h)
+        h = self.resnet(h, temb, "mid_block.resnets.0")
+        h = self.transformer(h, ctx, "mid_block.attentions.0")
+        h = self.resnet(h, temb, "mid_block.resnets.1")
+        for i, typ in enumerate(cfg.up_block_types):
+            for j in range(L + 1):
+                h = torch.cat([h, skips.pop()], dim=1)
+                h = self.resnet(h, temb, f"up_blocks.{i}.resnets.{j}")
+                if typ.startswith("CrossAttn"):
+                    h = self.transformer(h, ctx, f"up_blocks.{i}.attentions.{j}")
+            if i < nblk - 1:
+                h = F.interpolate(h, scale_factor=2.0, mode="nearest")
+                h = self.conv(h, f"up_blocks.{i}.upsamplers.0.conv")
+        h = F.silu(self.gn(h, "conv_norm_out", cfg.norm_eps))
+        return self.conv(h, "conv_out")
+
+
+def ddim_schedule(num_inference_steps=50, num_train_timesteps=1000, beta_start=0.00085, beta_end=0.012,
+                  steps_offset=1, set_alpha_to_one=False):
+    """DDIMScheduler(beta_schedule='scaled_linear', timestep_spacing='leading') as configured by SD-1.x."""
+    betas = torch.linspace(beta_start ** 0.5, beta_end ** 0.5, num_train_timesteps, dtype=torch.float32) ** 2
+    alphas_cumprod = torch.cumprod(1.0 - betas, dim=0)
+    final = torch.tensor(1.0) if set_alpha_to_one else alphas_cumprod[0]
+    ratio = num_train_timesteps // num_inference_steps
+    ts = (np.arange(0, num_inference_steps) * ratio).round()[::-1].copy().astype(np.int64) + steps_offset
+    a_t = [float(alphas_cumprod[t]) for t in ts]
+    a_prev = [float(alphas_cumprod[t - ratio]) if t - ratio >= 0 else float(final) for t in ts]
+    return ts, a_t, a_prev
+
+
+def denoise(unet: UNetRef, latents, ctx_uncond, ctx_cond, num_inference_steps=50, guidance_scale=7.5,
+            ff_hook_factory=None, down_hook_factory=None, steps=None):
+    """StableDiffusionPipeline.__call__'s loop with DDIM + CFG (uncond first). Hook factories take the step
+    index and return the (layer, ...) hook for that U-Net call — the reference's (t, l) counter."""
+    ts, a_t, a_prev = ddim_schedule(num_inference_steps)
+    x = latents.float().clone()
+    B = x.shape[0]
+    ctx = torch.cat([ctx_uncond, ctx_cond]).float()
+    nsteps = len(ts) if steps is None else steps
+    for s in range(nsteps):
+        inp = torch.cat([x, x])
+        ffh = ff_hook_factory(s) if ff_hook_factory else None
+        dh = down_hook_factory(s) if down_hook_factory else None
+        eps = unet(inp, float(ts[s]), ctx, ff_hook=ffh, down_hook=dh)
+        eu, ec = eps[:B], eps[B:]
+        e = eu + guidance_scale * (ec - eu)
+        x0 = (x - math.sqrt(1 - a_t[s]) * e) / math.sqrt(a_t[s])
+        x = math.sqrt(a_prev[s]) * x0 + math.sqrt(1 - a_prev[s]) * e
+    return x

@@ -1,0 +1,211 @@
+"""Per-kernel numerics of libsdmoe_hip.so on the MI355X against plain PyTorch fp32 references of the same op.
+
+Tolerances (fp16 storage, fp32 accumulation): max |out - ref| <= TOL * max(1, max |ref|) with TOL = 1e-2 for
+GEMM/conv/attention outputs (fp16 output rounding is 2^-11 relative; K up to 11520 adds accumulation-order
+differences), 2e-3 for the normalisation statistics.
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from sdmoe import ops  # noqa: E402
+
+DEV = "cuda"
+TOL = 1e-2
+
+
+def close(out, ref, tol=TOL):
+    out, ref = out.float(), ref.float()
+    err = (out - ref).abs().max().item()
+    scale = max(1.0, ref.abs().max().item())
+    assert math.isfinite(err) and err <= tol * scale, f"max err {err:.4g} vs scale {scale:.4g}"
+
+
+def rnd(*shape, scale=1.0, dtype=torch.float16, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(DEV, dtype)
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 320, 320), (130, 640, 768), (4096, 2560, 320), (64, 1280, 5120),
+                                   (1, 1280, 320), (1000, 960, 320), (77, 1280, 768)])
+def test_linear_bias_residual(M, N, K):
+    x = rnd(M, K, seed=1)
+    w = rnd(N, K, scale=K ** -0.5, seed=2)
+    b = rnd(N, scale=0.1, seed=3)
+    r = rnd(M, N, seed=4)
+    out = ops.linear(x, w, b, residual=r)
+    ref = x.float() @ w.float().t() + b.float() + r.float()
+    close(out, ref)
+
+
+@pytest.mark.parametrize("act,fn", [(ops.ACT_SILU, F.silu), (ops.ACT_GELU, F.gelu), (ops.ACT_RELU, F.relu)])
+def test_linear_act(act, fn):
+    x, w, b = rnd(512, 640, seed=5), rnd(1280, 640, scale=640 ** -0.5, seed=6), rnd(1280, scale=0.1, seed=7)
+    close(ops.linear(x, w, b, act=act), fn(x.float() @ w.float().t() + b.float()))
+
+
+def test_linear_strided_views():
+    """Row-strided input/output views (zero-copy concat slices, fused QKV columns)."""
+    big = rnd(300, 960, seed=8)
+    x = big[:, 320:640]
+    w = rnd(640, 320, scale=320 ** -0.5, seed=9)
+    dst = torch.zeros(300, 1000, dtype=torch.float16, device=DEV)
+    ops.linear(x, w, out=dst[:, 200:840])
+    close(dst[:, 200:840], x.float() @ w.float().t())
+    assert dst[:, :200].abs().max().item() == 0 and dst[:, 840:].abs().max().item() == 0
+
+
+def test_linear_groupnorm_apply_and_coladd():
+    nimg, HW, C, N = 3, 64, 320, 640
+    x = rnd(nimg * HW, C, seed=10)
+    gamma, beta = rnd(C, scale=0.1, seed=11) + 1, rnd(C, scale=0.1, seed=12)
+    sc, sh = ops.groupnorm_stats(x, nimg, HW, gamma, beta, 1e-6, 32)
+    w, b = rnd(N, C, scale=C ** -0.5, seed=13), rnd(N, scale=0.1, seed=14)
+    col = rnd(nimg, N, seed=15)
+    out = ops.linear(x, w, b, gn=(sc, sh, True), rows_per_batch=HW, coladd=col, coladd_bstride=N)
+    xn = F.group_norm(x.float().view(nimg, HW, C).permute(0, 2, 1), 32, gamma.float(), beta.float(), 1e-6)
+    xn = F.silu(xn.permute(0, 2, 1).reshape(nimg * HW, C))
+    ref = xn @ w.float().t() + b.float() + col.float().repeat_interleave(HW, 0)
+    close(out, ref)
+
+
+def test_linear_wanda_bitmask():
+    M, N, K = 256, 320, 1280
+    x, w, b = rnd(M, K, seed=16), rnd(N, K, scale=K ** -0.5, seed=17), rnd(N, scale=0.1, seed=18)
+    g = torch.Generator().manual_seed(19)
+    mask = (torch.rand(N, K, generator=g) < 0.03).to(torch.uint8)
+    import numpy as np
+    bits = torch.from_numpy(np.packbits(mask.numpy(), axis=-1, bitorder="little")).to(DEV)
+    out = ops.linear(x, w, b, wmask_bits=bits)
+    ref = x.float() @ (w.float() * (1 - mask.to(DEV).float())).t() + b.float()
+    close(out, ref)
+
+
+def conv_ref(x, nimg, H, W, w, b, stride=1, upsample=False):
+    xc = x.float().view(nimg, H, W, -1).permute(0, 3, 1, 2)
+    if upsample:
+        xc = F.interpolate(xc, scale_factor=2.0, mode="nearest")
+    wc = w.float().permute(0, 3, 1, 2)
+    y = F.conv2d(xc, wc, b.float(), stride=stride, padding=1)
+    return y.permute(0, 2, 3, 1).reshape(-1, w.shape[0])
+
+
+@pytest.mark.parametrize("Cin,Cout,H,stride,up", [(64, 320, 16, 1, False), (320, 320, 16, 1, False),
+                                                  (320, 320, 16, 2, False), (640, 640, 8, 1, True),
+                                                  (960, 320, 8, 1, False), (320, 8, 16, 1, False),
+                                                  (1280, 1280, 8, 1, False)])
+def test_conv3x3(Cin, Cout, H, stride, up):
+    nimg = 2
+    x = rnd(nimg * H * H, Cin, seed=20)
+    w = rnd(Cout, 3, 3, Cin, scale=(9 * Cin) ** -0.5, seed=21)
+    b = rnd(Cout, scale=0.1, seed=22)
+    out = ops.conv3x3(x, nimg, H, H, w, b, stride=stride, upsample=up)
+    close(out, conv_ref(x, nimg, H, H, w, b, stride, up))
+
+
+def test_conv3x3_gn_silu_temb_residual():
+    nimg, H, Cin, Cout = 2, 16, 320, 640
+    x = rnd(nimg * H * H, Cin, seed=23)
+    gamma, beta = rnd(Cin, scale=0.1, seed=24) + 1, rnd(Cin, scale=0.1, seed=25)
+    sc, sh = ops.groupnorm_stats(x, nimg, H * H, gamma, beta, 1e-5, 32)
+    w, b = rnd(Cout, 3, 3, Cin, scale=(9 * Cin) ** -0.5, seed=26), rnd(Cout, scale=0.1, seed=27)
+    temb = rnd(1, Cout, seed=28)
+    res = rnd(nimg * H * H, Cout, seed=29)
+    out = ops.conv3x3(x, nimg, H, H, w, b, gn=(sc, sh, True), coladd=temb, coladd_bstride=0, residual=res)
+    xn = F.group_norm(x.float().view(nimg, H * H, Cin).permute(0, 2, 1), 32, gamma.float(), beta.float(), 1e-5)
+    xn = F.silu(xn).permute(0, 2, 1).reshape(-1, Cin)
+    ref = conv_ref(xn, nimg, H, H, w, b) + temb.float() + res.float()
+    close(out, ref)
+
+
+def test_conv3x3_strided_concat_input():
+    nimg, H, C1, C2, Cout = 2, 8, 640, 320, 320
+    buf = rnd(nimg * H * H, C1 + C2, seed=30)
+    w, b = rnd(Cout, 3, 3, C1 + C2, scale=(9 * (C1 + C2)) ** -0.5, seed=31), rnd(Cout, scale=0.1, seed=32)
+    close(ops.conv3x3(buf, nimg, H, H, w, b), conv_ref(buf, nimg, H, H, w, b))
+    w2 = rnd(Cout, 3, 3, C2, scale=(9 * C2) ** -0.5, seed=33)
+    close(ops.conv3x3(buf[:, C1:], nimg, H, H, w2, b), conv_ref(buf[:, C1:].contiguous(), nimg, H, H, w2, b))
+
+
+@pytest.mark.parametrize("C,HW,eps", [(320, 4096, 1e-5), (960, 256, 1e-6), (2560, 64, 1e-5), (1920, 1024, 1e-5)])
+def test_groupnorm_stats(C, HW, eps):
+    nimg = 2
+    x = rnd(nimg * HW, C, seed=34) * 2 + 3  # non-zero mean exercises the shifted sums
+    gamma, beta = rnd(C, scale=0.1, seed=35) + 1, rnd(C, scale=0.1, seed=36)
+    sc, sh = ops.groupnorm_stats(x, nimg, HW, gamma, beta, eps, 32)
+    xn = x.float().view(nimg, HW, C) * sc[:, None, :] + sh[:, None, :]
+    ref = F.group_norm(x.float().view(nimg, HW, C).permute(0, 2, 1), 32, gamma.float(), beta.float(), eps)
+    close(xn, ref.permute(0, 2, 1), tol=2e-3)
+
+
+@pytest.mark.parametrize("C", [320, 640, 1280])
+def test_layernorm(C):
+    x = rnd(777, C, seed=37) * 3 + 1
+    g, b = rnd(C, scale=0.1, seed=38) + 1, rnd(C, scale=0.1, seed=39)
+    close(ops.layernorm(x, g, b, 1e-5), F.layer_norm(x.float(), (C,), g.float(), b.float(), 1e-5), tol=5e-3)
+
+
+@pytest.mark.parametrize("d,Nq,Nk", [(40, 256, 256), (40, 4096, 77), (80, 1024, 1024), (80, 200, 77),
+                                     (160, 256, 256), (160, 64, 77), (64, 300, 300)])
+def test_attention(d, Nq, Nk):
+    nimg, heads = 2, 8
+    C = heads * d
+    qkv = rnd(nimg * Nq, 3 * C, seed=40)
+    kv = rnd(nimg * Nk, 2 * C, seed=41)
+    if Nk == Nq:
+        q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
+    else:
+        q, k, v = qkv[:, :C], kv[:, :C], kv[:, C:]
+    out = ops.attention(q, k, v, nimg, Nq, Nk, heads)
+    qf = q.float().reshape(nimg, Nq, heads, d).transpose(1, 2)
+    kf = k.float().reshape(nimg, Nk, heads, d).transpose(1, 2)
+    vf = v.float().reshape(nimg, Nk, heads, d).transpose(1, 2)
+    ref = F.scaled_dot_product_attention(qf, kf, vf).transpose(1, 2).reshape(nimg * Nq, C)
+    close(out, ref)
+
+
+def test_attention_peaked_softmax():
+    """A spiked key forces the online-softmax rescale branch at a later tile."""
+    nimg, heads, d, N = 1, 8, 80, 512
+    C = heads * d
+    q = rnd(nimg * N, C, seed=42)
+    k = rnd(nimg * N, C, seed=43)
+    k[300] = q[5] * 4  # query 5 now peaks at key 300 (tile 4)
+    v = rnd(nimg * N, C, seed=44)
+    out = ops.attention(q, k, v, nimg, N, N, heads)
+    qf = q.float().view(1, N, heads, d).transpose(1, 2)
+    kf = k.float().view(1, N, heads, d).transpose(1, 2)
+    vf = v.float().view(1, N, heads, d).transpose(1, 2)
+    ref = F.scaled_dot_product_attention(qf, kf, vf).transpose(1, 2).reshape(N, C)
+    close(out, ref)
+
+
+def test_timestep_embedding():
+    import sys, os  # noqa: E401
+    from oracle.unet_ref import timestep_embedding
+    for t in (1.0, 481.0, 981.0):
+        out = ops.timestep_embedding(t, 320, DEV)
+        close(out, timestep_embedding(t, 320).to(DEV), tol=2e-3)
+
+
+def test_cfg_ddim_step_and_prepare():
+    B, H = 2, 16
+    lat = rnd(B, 4, H, H, dtype=torch.float32, seed=45)
+    eps = rnd(2 * B * H * H, 8, seed=46)
+    x_in = torch.zeros(2 * B * H * H, 64, dtype=torch.float16, device=DEV)
+    ops.prepare_input(lat, x_in, 2)
+    ref_in = lat.permute(0, 2, 3, 1).reshape(B * H * H, 4)
+    close(x_in[:B * H * H, :4], ref_in, tol=1e-3)
+    close(x_in[B * H * H:, :4], ref_in, tol=1e-3)
+    assert x_in[:, 4:].abs().max().item() == 0
+    a_t, a_p, g = 0.3, 0.5, 7.5
+    e = eps.float()[:, :4].reshape(2, B, H, H, 4).permute(0, 1, 4, 2, 3)
+    ee = e[0] + g * (e[1] - e[0])
+    x0 = (lat - math.sqrt(1 - a_t) * ee) / math.sqrt(a_t)
+    ref = math.sqrt(a_p) * x0 + math.sqrt(1 - a_p) * ee
+    ops.cfg_ddim_step(eps, lat, True, g, a_t, a_p, next_in=x_in)
+    close(lat, ref, tol=1e-4)

@@ -1,0 +1,184 @@
+"""U-Net / pipeline / receiver parity on the MI355X vs the fp32 CPU oracle (oracle/unet_ref.py).
+
+The oracle gets the same fp16-rounded weights, so differences come only from fp16 activations and fp32
+accumulation order. Tolerances:
+  * one U-Net evaluation, no routing: max|eps - ref| <= 3e-2 * max(1, max|ref|);
+  * multi-step denoising with MoE routing: relative L2 of the final latents <= 3e-2 (an fp16 near-tie can
+    flip one token's expert choice vs the fp32 oracle, which max-abs would over-weight).
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from sdmoe.config import UNetConfig  # noqa: E402
+from sdmoe.unet import UNet2DConditionModel  # noqa: E402
+from sdmoe.weights import make_state_dict  # noqa: E402
+from sdmoe.pipeline import StableDiffusionPipeline, prompt_embedding, initial_latents  # noqa: E402
+from oracle.unet_ref import UNetRef, denoise  # noqa: E402
+from oracle import hooks_ref as H  # noqa: E402
+
+DEV = "cuda"
+
+
+def rel_l2(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return ((a - b).norm() / b.norm()).item()
+
+
+def max_rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return (a - b).abs().max().item() / max(1.0, b.abs().max().item())
+
+
+def build(cfg, seed=0):
+    sd = make_state_dict(cfg, seed)
+    sd16 = {k: v.half().float() for k, v in sd.items()}
+    return UNet2DConditionModel.from_state_dict(sd, cfg, DEV), UNetRef(sd16, cfg)
+
+
+@pytest.fixture(scope="module")
+def tiny():
+    cfg = UNetConfig.tiny(16)
+    return (cfg,) + build(cfg)
+
+
+def ctx_for(cfg, prompts):
+    d = cfg.cross_attention_dim
+    return torch.stack([prompt_embedding("", d)] * len(prompts) + [prompt_embedding(p, d) for p in prompts])
+
+
+def test_unet_forward_tiny(tiny):
+    cfg, unet, ref = tiny
+    moefy_tiny(StableDiffusionPipeline(unet, DEV), topk=None)
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(2, 4, 16, 16, generator=g)
+    ctx = ctx_for(cfg, ["a photo of a cat"])
+    for t in (981.0, 501.0, 1.0):
+        eps = unet(x.to(DEV), t, ctx.to(DEV))
+        r = ref(x, t, ctx)
+        assert max_rel(eps, r) <= 3e-2, t
+
+
+def test_unet_forward_sd14_32x32():
+    cfg = UNetConfig.sd14(32)
+    unet, ref = build(cfg, seed=3)
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(2, 4, 32, 32, generator=g)
+    ctx = ctx_for(cfg, ["Starry night by Van Gogh"])
+    eps = unet(x.to(DEV), 741.0, ctx.to(DEV))
+    r = ref(x, 741.0, ctx)
+    assert max_rel(eps, r) <= 3e-2
+    assert 0.1 < r.std().item() < 10  # synthetic weights stay numerically tame
+    del unet
+
+
+def moefy_tiny(pipe, topk=0.25, expert_size=16, relu=True):
+    from moefication.helper import moefy_synthetic
+    from sparsity.relufy_model import find_and_change_geglu
+    from sdmoe.unet import GEGLU, _gelu
+    if topk is not None:
+        moefy_synthetic(pipe, topk, expert_size, seed=5)
+    for _, m in pipe.unet.named_modules():
+        if isinstance(m, GEGLU):
+            m.gelu = _gelu
+            if topk is None:
+                m.patterns = None
+    if topk is None:
+        return None
+    if relu:
+        find_and_change_geglu(pipe.unet)
+    mods = [m for n, m in pipe.unet.named_modules() if n.endswith("ff.net.0")]
+    return [(m.labels.numpy(), m.patterns.shape[0], m.k) for m in mods]
+
+
+def oracle_ff_hook_factory(layers, act, removed=None):
+    def factory(step):
+        def hook(layer, x, w, b):
+            labels, E, k = layers[layer]
+            P = H.patterns_from_labels(labels, torch.float32)
+            ids = removed[step][layer] if removed is not None else None
+            out, *_ = H.geglu_hook(x, w, b, P, k, act, removed=ids, apply_removal=step < 20)
+            return out
+        return hook
+    return factory
+
+
+def run_oracle(ref, cfg, prompts, steps, seed=0, **kw):
+    lat = torch.cat([initial_latents(seed, i, cfg) for i in range(len(prompts))])
+    d = cfg.cross_attention_dim
+    cu = torch.stack([prompt_embedding("", d)] * len(prompts))
+    cc = torch.stack([prompt_embedding(p, d) for p in prompts])
+    return denoise(ref, lat, cu, cc, num_inference_steps=steps, **kw)
+
+
+def test_pipeline_moefy_receiver_tiny(tiny):
+    from neuron_receivers import MOEFy
+    cfg, unet, ref = tiny
+    pipe = StableDiffusionPipeline(unet, DEV, num_inference_steps=4)
+    layers = moefy_tiny(pipe)
+    rec = MOEFy(seed=0)
+    prompts = ["a dog", "a painting of a river"]
+    out, gates = rec.observe_activation(pipe, prompts)
+    assert len(gates) == 4 * 16 and tuple(gates[0].shape) == (4, 256, 256)
+    assert all(bool(torch.all(g >= 0)) for g in gates)  # relufied
+    exp = run_oracle(ref, cfg, prompts, 4, ff_hook_factory=oracle_ff_hook_factory(layers, "relu"))
+    got = torch.stack(out)
+    assert rel_l2(got, exp) <= 3e-2
+    # per-token expert count: every stored gate row uses at most k experts' neurons
+    labels, E, k = layers[0]
+    g0 = gates[0].reshape(-1, 256).float()
+    active = torch.zeros(g0.shape[0], E)
+    lab = torch.from_numpy(labels)
+    active.index_add_(1, lab, (g0 != 0).float())
+    assert int(((active > 0).sum(1) <= k).all())
+
+
+def test_pipeline_remove_experts_receiver_tiny(tiny):
+    from neuron_receivers import GEGLU, RemoveExperts
+    cfg, unet, ref = tiny
+    pipe = StableDiffusionPipeline(unet, DEV, num_inference_steps=3)
+    layers = moefy_tiny(pipe, relu=False)
+    g = torch.Generator().manual_seed(9)
+    T, L = 3, 16
+    lists = {t: {l: sorted(torch.randperm(layers[l][1], generator=g)[:max(1, layers[l][1] // 4)].tolist())
+                 for l in range(L)} for t in range(T)}
+    rec = RemoveExperts(0, None, T, L, replace_fn=GEGLU, expert_indices=lists, store_gates=False)
+    out, gates = rec.observe_activation(pipe, ["a church"])
+    assert gates == [] and (rec.timestep, rec.layer) == (3, 0)
+    exp = run_oracle(ref, cfg, ["a church"], 3, ff_hook_factory=oracle_ff_hook_factory(layers, "gelu", lists))
+    assert rel_l2(out, exp[0]) <= 3e-2
+
+
+def test_pipeline_wanda_union_receiver_tiny(tiny):
+    import numpy as np
+    from neuron_receivers import WandaRemoveNeuronsFast, MultiConceptRemoverWanda
+    cfg, unet, ref = tiny
+    pipe = StableDiffusionPipeline(unet, DEV, num_inference_steps=2)
+    moefy_tiny(pipe, topk=None)
+    downs = [m for n, m in pipe.unet.named_modules() if n.endswith("ff.net.2")]
+    T, L = 2, 16
+    rng = np.random.default_rng(0)
+    concepts = {}
+    for c in ("church", "parachute"):
+        concepts[c] = {t: {l: (rng.random(tuple(downs[l].weight.shape)) < 0.03).astype(np.int64) for l in range(L)}
+                       for t in range(T)}
+    removers = {c: WandaRemoveNeuronsFast(0, None, T, L, masks=m, store_gates=False) for c, m in concepts.items()}
+    mc = MultiConceptRemoverWanda(None, 0, T, L, concepts_to_remove=list(concepts), removers=removers)
+    mc.handle_multiple_concepts(list(concepts))
+    union = {t: {l: H.union_masks([concepts[c][t][l] for c in concepts]) for l in range(L)} for t in range(T)}
+    for t in range(T):
+        for l in range(L):
+            assert np.array_equal(mc.union_neuron_remover.dense_mask(t, l), union[t][l])
+    u = mc.union_neuron_remover
+    u.reset_time_layer()
+    out, _ = u.observe_activation(pipe, "a parachute over a church")
+
+    def down_factory(step):
+        def hook(layer, x, w, b):
+            return H.wanda_linear(x, w, b, union[step][layer])
+        return hook
+    exp = run_oracle(ref, cfg, ["a parachute over a church"], 2, down_hook_factory=down_factory)
+    assert rel_l2(out, exp[0]) <= 3e-2
