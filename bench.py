@@ -70,20 +70,13 @@ def synth_expert_lists(num_experts, T, seed=7):
     return out
 
 
-def broadcast_obj(obj, world, rank):
-    if world == 1:
-        return obj
-    lst = [obj if rank == 0 else None]
-    dist.broadcast_object_list(lst, src=0)
-    return lst[0]
-
-
 def build(args, world, rank, dev):
     from sdmoe.config import UNetConfig
     from sdmoe.pipeline import StableDiffusionPipeline
     from moefication.helper import moefy_synthetic
     from sparsity.relufy_model import find_and_change_geglu
     from neuron_receivers import RemoveExperts, MOEFy, WandaRemoveNeuronsFast
+    from sdmoe import distributed as D
 
     cfg = UNetConfig.sd14(64)
     pipe = StableDiffusionPipeline.synthetic(cfg, seed=0, device=dev, num_inference_steps=args.inference_steps)
@@ -95,8 +88,8 @@ def build(args, world, rank, dev):
     if args.mask == "none":
         rec = MOEFy(seed=0, store_gates=False)
     else:
-        lists = broadcast_obj(synth_expert_lists([m.patterns.shape[0] for m in geglus], T) if rank == 0 else None,
-                              world, rank)
+        lists = D.broadcast_object(synth_expert_lists([m.patterns.shape[0] for m in geglus], T) if rank == 0
+                                   else None)
         rec = RemoveExperts(0, None, T, len(geglus), expert_indices=lists, store_gates=False)
     wanda = None
     if args.mask == "union":
@@ -117,9 +110,8 @@ def build(args, world, rank, dev):
                     b = (m.view(shape[0], shape[1] // 8, 8).to(torch.uint8) * weights8).sum(-1, dtype=torch.uint8)
                 else:
                     b = torch.empty((shape[0], shape[1] // 8), dtype=torch.uint8, device=dev)
-                if world > 1:
-                    dist.broadcast(b, src=0)
                 bits[t][l] = b.contiguous()
+        D.broadcast_tensors([bits[t][l] for t in range(T) for l in range(len(downs))])  # once, over RCCL
         wanda = WandaRemoveNeuronsFast.from_packed(0, {t: {l: np.zeros((1, 1), np.uint8) for l in range(len(downs))}
                                                        for t in range(T)}, T, len(downs), store_gates=False)
         for t in range(T):
@@ -222,8 +214,9 @@ def main():
     _lib.load()
     cfg, pipe, rec, wanda = build(args, world, rank, dev)
     # global prompt list: rank r takes its contiguous shard (per-prompt seeds use the global index)
+    from sdmoe import distributed as D
     prompts = [f"synthetic prompt {i}" for i in range(world * args.batch)]
-    mine = prompts[rank * args.batch:(rank + 1) * args.batch]
+    mine, offset = D.shard(prompts, rank, world)
 
     timer = KernelTimer("conv3x3")
     if not args.no_roofline:
@@ -231,7 +224,7 @@ def main():
     pipe.unet.conv_in.weight._sdmoe_conv_in = True
     pipe.unet.conv_out.weight._sdmoe_conv_out = True
 
-    pipe.prompt_offset = rank * args.batch  # global prompt index of this rank's first prompt
+    pipe.prompt_offset = offset  # global prompt index of this rank's first prompt (seeds its latents)
 
     def one_step():
         """One batch through the reference receiver API: observe_activation(pipe, prompts)."""
@@ -263,10 +256,7 @@ def main():
     timer.active = False
     if world > 1:
         dist.barrier()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    elapsed = float(elapsed.item())
+    elapsed = D.max_over_ranks(t1 - t0, dev)
     finite = all(bool(torch.isfinite(x).all()) for x in imgs)
     images = world * args.batch * args.steps
     value = images / elapsed

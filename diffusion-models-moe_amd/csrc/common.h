@@ -33,7 +33,9 @@ SDMOE_DEV float4v mfma16x16x32(half8 a, half8 b, float4v c) {
 }
 
 SDMOE_DEV float silu_f(float x) { return x / (1.0f + __expf(-x)); }
-SDMOE_DEV float gelu_erf_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+// exact-erf GELU written through erfc so the negative tail keeps full relative precision (1 + erf(x/sqrt2)
+// cancels in fp32 below x ~ -3); within 1 fp16 ulp of the correctly rounded value.
+SDMOE_DEV float gelu_erf_f(float x) { return 0.5f * x * erfcf(-x * 0.70710678118654752f); }
 
 SDMOE_DEV float wave_sum(float v) {
 #pragma unroll

@@ -1,25 +1,32 @@
 // MFMA GEMM / implicit-GEMM 3x3 convolution for gfx950, fp16 in / fp32 accumulate / fp16 out.
 //
 // One kernel template covers every dense projection of the SD U-Net step:
-//   * Linear layers (attention q/k/v/out, proj_in/proj_out 1x1 convs, GEGLU proj, FFN down-proj,
-//     time-embedding MLP)  -- MODE_GEMM, activations [M, K] row-major, weights [N, K] (nn.Linear layout);
-//   * ResNet 3x3 convolutions (stride 1/2, fused nearest-2x upsample) on NHWC activations -- MODE_CONV,
-//     weights [Cout][3][3][Cin] so K = 9*Cin is contiguous per output channel.
-// Fusions (all optional, chosen per launch):
-//   A-load : GroupNorm apply (per (image, channel) fp32 scale/shift) + SiLU, done in registers while the
-//            tile is staged to LDS (zero padding stays zero, as in F.conv2d on the normalised tensor);
-//   B-load : Wanda weight bitmask (bit = 1 -> weight zeroed), replacing the reference's per-call
-//            W.clone()*(1-M) (remove_wanda_neurons_fast.py:69-83);
-//   epilogue: + bias[n] + coladd[image][n] (time embedding) -> activation -> + residual[m][n].
-// Tiles: BMxBNx64, 256 threads = 2x2 waves, 16x16x32 f16 MFMA, register-staged double-buffered LDS with an
-// XOR chunk swizzle (conflict-free ds_read_b128 for 16 consecutive rows), fp32 epilogue staged through LDS
-// so global stores are 16 B per lane.
+//   * Linear layers (attention q/k/v/out, proj_in/proj_out 1x1 convs, GEGLU proj, FFN down-proj, time MLP):
+//     activations [M, K] row-major (any row stride), weights [N, K] (nn.Linear layout);
+//   * ResNet 3x3 convolutions (stride 1/2, fused nearest-2x upsample) on NHWC activations: weights
+//     [Cout][3][3][Cin] so K = 9*Cin is contiguous per output channel and every 64-wide K-step is one tap.
+// Main loop: 256 threads = 2x2 waves, BK = 64, 16x16x32 f16 MFMA. Both operand tiles go HBM -> LDS with
+// global_load_lds_dwordx4 (LDS-DMA, no register staging), one 1-KiB wave-instruction per 8 rows; conv halo
+// rows and M/N tails point at a zero line. A 3-stage LDS ring keeps two K-steps in flight behind a counted
+// `s_waitcnt vmcnt` and one raw s_barrier per K-step. The LDS image is XOR-swizzled by pre-swizzling the
+// per-lane SOURCE chunk (LDS-DMA writes lane-linearly), so 16 consecutive rows read conflict-free.
+// BN = 160 divides every SD channel count (320*k), so N = 320/640/1280/2560/... tiles exactly.
+// Small grids (8x8 / 16x16 latents, K up to 23040) split K over workgroups: fp32 partial slabs + a
+// deterministic ordered reduce kernel that also runs the epilogue.
+// Epilogue (fused): + bias[n] + coladd[image][n] (time embedding) -> activation -> + residual[m][n],
+// staged through LDS so stores are 16 B per lane.
 #include "common.h"
 #include "../../include/sdmoe.h"
 
 namespace {
 
 constexpr int BK = 64;
+
+// tuning knobs (sdmoe_tune): 0 = LDS stages (0 = auto, 2 or 3)
+int g_stages = 0;
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
 
 struct GemmParams {
   const half_t* A; long lda;
@@ -28,144 +35,163 @@ struct GemmParams {
   const half_t* coladd; long coladd_bstride;
   const half_t* R; long ldr;
   half_t* C; long ldc;
+  float* part;  // split-K partial slabs [ksplit][M][N] fp32 (ld N), or null
   int M, N, K;
   int act;
-  const float* a_scale; const float* a_shift; int a_silu; int a_chan;  // a_chan: channels per image row
   int rows_per_batch;
   int H, Wd, Cin, OH, OW, stride, upsample;
-  const uint8_t* wmask;  // [N][K/8] bytes
+  int ksplit, kchunk;
+  int a_bytes, w_bytes;  // SRD num_records
 };
 
-SDMOE_DEV int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+SDMOE_DEV int swz(int row) { return (row >> 1) & 7; }
 
-template <int BM, int BN, bool CONV, bool ATRANS, bool WMASK>
-__global__ __launch_bounds__(256, 2) void gemm_kernel(GemmParams p) {
+constexpr unsigned OOB = 0x80000000u;  // > every num_records used here (tensors < 2 GiB)
+
+SDMOE_DEV void bld16(__amdgpu_buffer_rsrc_t rs, char* lds_dst, unsigned voff, unsigned soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)lds_dst, 16, voff, soff, 0, 0);
+}
+
+// shared epilogue for one 8-column chunk: v += bias, coladd; act; + residual; store fp16
+SDMOE_DEV void epilogue8(const GemmParams& p, int m, int n, float (&v)[8]) {
+  if (p.bias) {
+    half8 bb = *reinterpret_cast<const half8*>(p.bias + n);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] += (float)bb[j];
+  }
+  if (p.coladd) {
+    const int b = m / p.rows_per_batch;
+    half8 cc = *reinterpret_cast<const half8*>(p.coladd + (long)b * p.coladd_bstride + n);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] += (float)cc[j];
+  }
+  if (p.act != ACT_NONE) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = apply_act(v[j], p.act);
+  }
+  if (p.R) {
+    half8 rr = *reinterpret_cast<const half8*>(p.R + (long)m * p.ldr + n);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] += (float)rr[j];
+  }
+  half8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (half_t)v[j];
+  *reinterpret_cast<half8*>(p.C + (long)m * p.ldc + n) = o;
+}
+
+enum { MODE_GEMM = 0, MODE_CONV = 1, MODE_CONV_UP = 2 };
+
+template <int BM, int BN, int MODE, int NSTAGE>
+__global__ __launch_bounds__(256, (NSTAGE == 2 ? 2 : 1)) void gemm_kernel(GemmParams p) {
+  constexpr bool CONV = MODE != MODE_GEMM;
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int FM = WM / 16, FN = WN / 16;
-  constexpr int A_PER = BM / 32, B_PER = BN / 32;
-  constexpr int STAGE_BYTES = 2 * (BM + BN) * BK * 2;
+  constexpr int A_PW = BM / 32, B_PW = BN / 32;  // LDS-DMA wave-instructions (8 rows each) per wave and stage
+  constexpr int PER_WAVE = A_PW + B_PW;
+  constexpr int STAGE = (BM + BN) * BK * 2;
   constexpr int WN_PAD = WN + 4;
-  constexpr int EPI_BYTES = 4 * WM * WN_PAD * 4;
-  constexpr int SMEM = STAGE_BYTES > EPI_BYTES ? STAGE_BYTES : EPI_BYTES;
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];
-  half_t* sA = reinterpret_cast<half_t*>(smem);
-  half_t* sB = sA + 2 * BM * BK;
+  constexpr int EPI = 4 * (WM / 2) * WN_PAD * 4;
+  constexpr int SMEM = (NSTAGE * STAGE > EPI) ? NSTAGE * STAGE : EPI;
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 1, wc = wave & 1;
   const int ntn = (p.N + BN - 1) / BN, ntm = (p.M + BM - 1) / BM;
-  const int bid = xcd_remap(blockIdx.x, ntn * ntm);
-  const int tn = bid % ntn, tm = bid / ntn;
+  const int bid = xcd_remap(blockIdx.x, ntn * ntm * p.ksplit);
+  const int split = bid % p.ksplit, tile = bid / p.ksplit;
+  const int tn = tile % ntn, tm = tile / ntn;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int nk = p.K / BK;
+  const int nk_total = p.K / BK;
+  const int ks0 = split * p.kchunk;
+  const int ks1 = min(nk_total, ks0 + p.kchunk);
+  const int nk = ks1 - ks0;
 
-  // per-thread staging rows (fixed for the whole K loop)
-  int a_row[A_PER], a_kc[A_PER];
-  int a_b[A_PER], a_oh[A_PER], a_ow[A_PER];
-  bool a_ok[A_PER];
+  // ---- LDS-DMA sources: buffer loads through two SRDs (A, W); an out-of-range offset (OOB) is dropped by the
+  // hardware range check and lands as zeros, which gives conv halo rows and M/N tails for free.
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsW = __builtin_amdgcn_make_buffer_rsrc((void*)p.W, (short)0, p.w_bytes, 0x00020000);
+  const int lrow = lane >> 3, lch = lane & 7;
+  // A rows: wave w stages rows [8*(w*A_PW + j), +8); B rows likewise with B_PW
+  unsigned avoff[A_PW];  // GEMM: byte offset of (row, pre-swizzled chunk); conv: of the centre-tap pixel
+  unsigned amask[A_PW];  // conv: bit t = tap t in bounds (0 = M-tail row)
+  int aoh[A_PW], aow[A_PW], ab_[A_PW];  // conv-upsample rows
+  unsigned bvoff[B_PW];
 #pragma unroll
-  for (int i = 0; i < A_PER; ++i) {
-    int id = tid + 256 * i;
-    a_row[i] = id >> 3; a_kc[i] = id & 7;
-    int m = m0 + a_row[i];
-    a_ok[i] = m < p.M;
-    int mm = a_ok[i] ? m : 0;
-    if (CONV) {
-      int hw = p.OH * p.OW;
-      a_b[i] = mm / hw; int r = mm - a_b[i] * hw;
-      a_oh[i] = r / p.OW; a_ow[i] = r - a_oh[i] * p.OW;
-    } else {
-      a_b[i] = ATRANS ? mm / p.rows_per_batch : 0; a_oh[i] = 0; a_ow[i] = 0;
-    }
-  }
-  int b_row[B_PER], b_kc[B_PER];
-  bool b_ok[B_PER];
-#pragma unroll
-  for (int i = 0; i < B_PER; ++i) {
-    int id = tid + 256 * i;
-    b_row[i] = id >> 3; b_kc[i] = id & 7;
-    b_ok[i] = (n0 + b_row[i]) < p.N;
-  }
-
-  uint4v ra[A_PER], rb[B_PER];
-
-  auto load_stage = [&](int ks) {
-    const int k0 = ks * BK;
-    int tap = 0, c0 = k0;
-    if (CONV) { tap = k0 / p.Cin; c0 = k0 - tap * p.Cin; }
-    const int kh = tap / 3, kw = tap - (tap / 3) * 3;
-#pragma unroll
-    for (int i = 0; i < A_PER; ++i) {
-      uint4v v = {0u, 0u, 0u, 0u};
-      bool ok = a_ok[i];
-      const half_t* src = nullptr;
-      if (CONV) {
-        int ih, iw;
-        if (p.upsample) {
-          int uh = a_oh[i] + kh - 1, uw = a_ow[i] + kw - 1;
-          ok = ok && uh >= 0 && uh < 2 * p.H && uw >= 0 && uw < 2 * p.Wd;
-          ih = uh >> 1; iw = uw >> 1;
-        } else {
-          ih = a_oh[i] * p.stride + kh - 1; iw = a_ow[i] * p.stride + kw - 1;
-          ok = ok && ih >= 0 && ih < p.H && iw >= 0 && iw < p.Wd;
-        }
-        if (ok) src = p.A + ((long)(a_b[i] * p.H + ih) * p.Wd + iw) * p.lda + c0 + a_kc[i] * 8;
+  for (int j = 0; j < A_PW; ++j) {
+    const int r = 8 * (wave * A_PW + j) + lrow;
+    const unsigned chb = (unsigned)((lch ^ swz(r)) * 16);
+    const int m = m0 + r;
+    avoff[j] = OOB; amask[j] = 0; aoh[j] = 0; aow[j] = 0; ab_[j] = 0;
+    if (m < p.M) {
+      if (MODE == MODE_GEMM) {
+        avoff[j] = (unsigned)((long)m * p.lda * 2) + chb;
       } else {
-        if (ok) src = p.A + (long)(m0 + a_row[i]) * p.lda + k0 + a_kc[i] * 8;
-      }
-      if (ok) {
-        v = *reinterpret_cast<const uint4v*>(src);
-        if (ATRANS) {
-          const int c = c0 + a_kc[i] * 8;
-          const float* sc = p.a_scale + (long)a_b[i] * p.a_chan + c;
-          const float* sh = p.a_shift + (long)a_b[i] * p.a_chan + c;
-          float4v s0 = *reinterpret_cast<const float4v*>(sc), s1 = *reinterpret_cast<const float4v*>(sc + 4);
-          float4v h0 = *reinterpret_cast<const float4v*>(sh), h1 = *reinterpret_cast<const float4v*>(sh + 4);
-          half8 x = __builtin_bit_cast(half8, v);
-          float s[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
-          float h[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+        const int hw = p.OH * p.OW;
+        const int b = m / hw, rr = m - b * hw;
+        const int oh = rr / p.OW, ow = rr - oh * p.OW;
+        if (MODE == MODE_CONV) {
+          const int ih = oh * p.stride, iw = ow * p.stride;  // centre tap (kh = kw = 1)
+          avoff[j] = (unsigned)(((long)(b * p.H + ih) * p.Wd + iw) * p.lda * 2) + chb;
+          unsigned msk = 0;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            float f = (float)x[j] * s[j] + h[j];
-            if (p.a_silu) f = silu_f(f);
-            x[j] = (half_t)f;
+          for (int t = 0; t < 9; ++t) {
+            const int y = ih + t / 3 - 1, x = iw + t % 3 - 1;
+            msk |= (y >= 0 && y < p.H && x >= 0 && x < p.Wd) ? (1u << t) : 0u;
           }
-          v = __builtin_bit_cast(uint4v, x);
+          amask[j] = msk;
+        } else {
+          amask[j] = 1; avoff[j] = chb; aoh[j] = oh; aow[j] = ow; ab_[j] = b;
         }
       }
-      ra[i] = v;
     }
+  }
 #pragma unroll
-    for (int i = 0; i < B_PER; ++i) {
-      uint4v v = {0u, 0u, 0u, 0u};
-      if (b_ok[i]) {
-        const long n = n0 + b_row[i];
-        const int k = k0 + b_kc[i] * 8;
-        v = *reinterpret_cast<const uint4v*>(p.W + n * p.ldw + k);
-        if (WMASK) {
-          unsigned bits = p.wmask[n * (p.K >> 3) + (k >> 3)];
-          if (bits) {
-            half8 x = __builtin_bit_cast(half8, v);
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-              if ((bits >> j) & 1u) x[j] = (half_t)0.0f;
-            v = __builtin_bit_cast(uint4v, x);
-          }
-        }
-      }
-      rb[i] = v;
-    }
-  };
+  for (int j = 0; j < B_PW; ++j) {
+    const int r = 8 * (wave * B_PW + j) + lrow;
+    const int n = n0 + r;
+    bvoff[j] = n < p.N ? (unsigned)((long)n * p.ldw * 2) + (unsigned)((lch ^ swz(r)) * 16) : OOB;
+  }
 
-  auto store_stage = [&](int buf) {
-    half_t* a = sA + buf * BM * BK;
-    half_t* b = sB + buf * BN * BK;
+  // conv K walk: (tap, 64-channel step) advanced incrementally in scalar registers
+  const int csteps = CONV ? p.Cin / BK : 1;
+  int st_tap = CONV ? ks0 / csteps : 0, st_c = CONV ? ks0 - st_tap * csteps : 0;
+
+  auto issue_stage = [&](int ks, int buf) {
+    char* sa = smem + buf * STAGE;
+    char* sbw = sa + BM * BK * 2;
+    const unsigned kb = (unsigned)(ks * BK * 2);
+    if (MODE == MODE_GEMM) {
 #pragma unroll
-    for (int i = 0; i < A_PER; ++i)
-      *reinterpret_cast<uint4v*>(a + a_row[i] * BK + swz(a_row[i], a_kc[i]) * 8) = ra[i];
+      for (int j = 0; j < A_PW; ++j) bld16(rsA, sa + (wave * A_PW + j) * 1024, avoff[j], kb);
+    } else {
+      const int tap = st_tap;
+      const int kh = tap >= 6 ? 2 : (tap >= 3 ? 1 : 0);
+      const int kw = tap - 3 * kh;
+      const int c0b = st_c * BK * 2;
+      if (++st_c == csteps) { st_c = 0; ++st_tap; }
+      if (MODE == MODE_CONV) {
+        const unsigned tapoff = (unsigned)(((kh - 1) * p.Wd + (kw - 1)) * (int)p.lda * 2 + c0b);
 #pragma unroll
-    for (int i = 0; i < B_PER; ++i)
-      *reinterpret_cast<uint4v*>(b + b_row[i] * BK + swz(b_row[i], b_kc[i]) * 8) = rb[i];
+        for (int j = 0; j < A_PW; ++j) {
+          const unsigned vo = ((amask[j] >> tap) & 1u) ? avoff[j] + tapoff : OOB;
+          bld16(rsA, sa + (wave * A_PW + j) * 1024, vo, 0);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < A_PW; ++j) {
+          const int uh = aoh[j] + kh - 1, uw = aow[j] + kw - 1;
+          const bool ok = amask[j] && uh >= 0 && uh < 2 * p.H && uw >= 0 && uw < 2 * p.Wd;
+          const unsigned vo =
+              ok ? (unsigned)(((long)(ab_[j] * p.H + (uh >> 1)) * p.Wd + (uw >> 1)) * p.lda * 2) + avoff[j] + c0b
+                 : OOB;
+          bld16(rsA, sa + (wave * A_PW + j) * 1024, vo, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < B_PW; ++j) bld16(rsW, sbw + (wave * B_PW + j) * 1024, bvoff[j], kb);
   };
 
   float4v acc[FM][FN];
@@ -174,103 +200,190 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmParams p) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = (float4v){0.f, 0.f, 0.f, 0.f};
 
-  load_stage(0);
-  store_stage(0);
-  __syncthreads();
+  // prologue: stages 0 .. NSTAGE-2
+#pragma unroll
+  for (int s = 0; s < NSTAGE - 1; ++s)
+    if (s < nk) issue_stage(ks0 + s, s);
 
   const int fr = lane & 15, fg = lane >> 4;
-  for (int ks = 0; ks < nk; ++ks) {
-    const int cur = ks & 1;
-    if (ks + 1 < nk) load_stage(ks + 1);
-    const half_t* a = sA + cur * BM * BK;
-    const half_t* b = sB + cur * BN * BK;
+  for (int it = 0; it < nk; ++it) {
+    // wait for this K-step's tile (leave the next one in flight), then make every wave's DMA visible
+    if (NSTAGE == 3 && it + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_WAVE) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (it + NSTAGE - 1 < nk) issue_stage(ks0 + it + NSTAGE - 1, (it + NSTAGE - 1) % NSTAGE);
+
+    const char* sa = smem + (it % NSTAGE) * STAGE;
+    const char* sbm = sa + BM * BK * 2;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       half8 af[FM], bf[FN];
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        int row = wr * WM + i * 16 + fr;
-        af[i] = *reinterpret_cast<const half8*>(a + row * BK + swz(row, kk * 4 + fg) * 8);
+        const int row = wr * WM + i * 16 + fr;
+        af[i] = *reinterpret_cast<const half8*>(sa + row * 128 + (((kk * 4 + fg) ^ swz(row)) << 4));
       }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        int row = wc * WN + j * 16 + fr;
-        bf[j] = *reinterpret_cast<const half8*>(b + row * BK + swz(row, kk * 4 + fg) * 8);
+        const int row = wc * WN + j * 16 + fr;
+        bf[j] = *reinterpret_cast<const half8*>(sbm + row * 128 + (((kk * 4 + fg) ^ swz(row)) << 4));
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32(af[i], bf[j], acc[i][j]);
     }
-    if (ks + 1 < nk) store_stage(cur ^ 1);
-    __syncthreads();
   }
 
-  // ---- epilogue: stage fp32 tile per wave, then 16-B vector stores with fused bias/coladd/act/residual
-  float* st = reinterpret_cast<float*>(smem) + wave * WM * WN_PAD;
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) st[(i * 16 + fg * 4 + r) * WN_PAD + j * 16 + fr] = acc[i][j][r];
+  // ---- epilogue: per wave, stage half of its fp32 tile (FM/2 fragment rows) in LDS at a time, then write
+  // 8-column chunks with 16-B (fp16) / 32-B (fp32 split-K slab) stores
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  constexpr int CPR = WN / 8;  // 8-column chunks per row
-  for (int id = lane; id < WM * CPR; id += 64) {
-    const int r = id / CPR, c8 = id - r * CPR;
-    const int m = m0 + wr * WM + r, n = n0 + wc * WN + c8 * 8;
-    if (m >= p.M || n >= p.N) continue;
-    const float* sp = st + r * WN_PAD + c8 * 8;
-    float4v v0 = *reinterpret_cast<const float4v*>(sp), v1 = *reinterpret_cast<const float4v*>(sp + 4);
-    float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-    if (p.bias) {
-      half8 bb = *reinterpret_cast<const half8*>(p.bias + n);
+  float* st = reinterpret_cast<float*>(smem) + wave * (WM / 2) * WN_PAD;
+  constexpr int CPR = WN / 8;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] += (float)bb[j];
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int i = 0; i < FM / 2; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) st[(i * 16 + fg * 4 + r) * WN_PAD + j * 16 + fr] = acc[h * (FM / 2) + i][j][r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int id = lane; id < (WM / 2) * CPR; id += 64) {
+      const int r = id / CPR, c8 = id - r * CPR;
+      const int m = m0 + wr * WM + h * (WM / 2) + r, n = n0 + wc * WN + c8 * 8;
+      if (m >= p.M || n >= p.N) continue;
+      const float* sp = st + r * WN_PAD + c8 * 8;
+      float4v v0 = *reinterpret_cast<const float4v*>(sp), v1 = *reinterpret_cast<const float4v*>(sp + 4);
+      if (p.part) {
+        float* dp = p.part + ((long)split * p.M + m) * p.N + n;
+        *reinterpret_cast<float4v*>(dp) = v0;
+        *reinterpret_cast<float4v*>(dp + 4) = v1;
+      } else {
+        float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+        epilogue8(p, m, n, v);
+      }
     }
-    if (p.coladd) {
-      const int b = m / p.rows_per_batch;
-      half8 cc = *reinterpret_cast<const half8*>(p.coladd + (long)b * p.coladd_bstride + n);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] += (float)cc[j];
-    }
-    if (p.act != ACT_NONE) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = apply_act(v[j], p.act);
-    }
-    if (p.R) {
-      half8 rr = *reinterpret_cast<const half8*>(p.R + (long)m * p.ldr + n);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] += (float)rr[j];
-    }
-    half8 o;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = (half_t)v[j];
-    *reinterpret_cast<half8*>(p.C + (long)m * p.ldc + n) = o;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 }
 
-template <int BM, int BN, bool CONV>
-int launch_tile(const GemmParams& p, hipStream_t s) {
-  const int blocks = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-  const bool at = p.a_scale != nullptr, wm = p.wmask != nullptr;
-  if (at && wm) gemm_kernel<BM, BN, CONV, true, true><<<blocks, 256, 0, s>>>(p);
-  else if (at) gemm_kernel<BM, BN, CONV, true, false><<<blocks, 256, 0, s>>>(p);
-  else if (wm) gemm_kernel<BM, BN, CONV, false, true><<<blocks, 256, 0, s>>>(p);
-  else gemm_kernel<BM, BN, CONV, false, false><<<blocks, 256, 0, s>>>(p);
+// split-K combine: ordered (deterministic) sum of the fp32 slabs + the fused epilogue
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
+  const long nchunk = (long)p.M * (p.N / 8);
+  for (long id = blockIdx.x * 256L + threadIdx.x; id < nchunk; id += (long)gridDim.x * 256) {
+    const int m = (int)(id / (p.N / 8)), n = (int)(id % (p.N / 8)) * 8;
+    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int s = 0; s < p.ksplit; ++s) {
+      const float* sp = p.part + ((long)s * p.M + m) * p.N + n;
+      float4v a = *reinterpret_cast<const float4v*>(sp), b = *reinterpret_cast<const float4v*>(sp + 4);
+      v[0] += a[0]; v[1] += a[1]; v[2] += a[2]; v[3] += a[3];
+      v[4] += b[0]; v[5] += b[1]; v[6] += b[2]; v[7] += b[3];
+    }
+    epilogue8(p, m, n, v);
+  }
+}
+
+template <int BM, int BN, int MODE>
+int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
+  const int ntiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+  const int nk = p.K / BK;
+  int ksplit = 1;
+  // fill the chip: split K when the tile grid covers well under one wave of 256 CUs
+  if (ws && ntiles < 192 && nk >= 16) {
+    ksplit = (256 + ntiles - 1) / ntiles;
+    if (ksplit > 8) ksplit = 8;
+    if (ksplit > nk / 4) ksplit = nk / 4;
+    while (ksplit > 1 && (long)ksplit * p.M * p.N > ws_floats) --ksplit;
+  }
+  p.ksplit = ksplit > 1 ? ksplit : 1;
+  p.kchunk = (nk + p.ksplit - 1) / p.ksplit;
+  p.part = p.ksplit > 1 ? ws : nullptr;
+  // 2-stage ring (2 workgroups/CU, latency hidden across workgroups) when the grid has >= ~300 workgroups;
+  // otherwise a 3-stage ring (1 workgroup/CU, two K-steps in flight) -- measured crossover on MI355X
+  int stages = g_stages ? g_stages : (ntiles * p.ksplit >= 300 ? 2 : 3);
+  if (stages == 2) gemm_kernel<BM, BN, MODE, 2><<<ntiles * p.ksplit, 256, 0, s>>>(p);
+  else gemm_kernel<BM, BN, MODE, 3><<<ntiles * p.ksplit, 256, 0, s>>>(p);
   SDMOE_CHECK_LAUNCH();
+  if (p.ksplit > 1) {
+    long nchunk = (long)p.M * (p.N / 8);
+    int g = (int)((nchunk + 255) / 256);
+    if (g > 2048) g = 2048;
+    splitk_reduce_kernel<<<g, 256, 0, s>>>(p);
+    SDMOE_CHECK_LAUNCH();
+  }
   return SDMOE_OK;
 }
 
-template <bool CONV>
-int dispatch(const GemmParams& p, hipStream_t s) {
-  // Pick the largest tile that still gives >= ~1 wave of blocks per CU (256 CUs).
-  const long t128 = (long)((p.M + 127) / 128) * ((p.N + 127) / 128);
-  const long t64x128 = (long)((p.M + 63) / 64) * ((p.N + 127) / 128);
-  if (p.N <= 64) return launch_tile<64, 64, CONV>(p, s);
-  if (t128 >= 240) return launch_tile<128, 128, CONV>(p, s);
-  if (t64x128 >= 240 || p.N < 128) return launch_tile<64, 128, CONV>(p, s);
-  return launch_tile<64, 64, CONV>(p, s);
+template <int MODE>
+int dispatch(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
+  if (MODE == MODE_CONV_UP) {  // only the 3 U-Net upsamplers: large M, N in {320, 640, 1280}
+    if (p.N % 160 == 0) return launch_tile<128, 160, MODE>(p, ws, ws_floats, s);
+    return launch_tile<128, 128, MODE>(p, ws, ws_floats, s);
+  }
+  const int nt160_128 = ((p.M + 127) / 128) * ((p.N + 159) / 160);
+  if (p.N <= 64) return launch_tile<128, 64, MODE>(p, ws, ws_floats, s);
+  if (p.N % 160 == 0) {
+    if (nt160_128 >= 200 || p.M > 2048) return launch_tile<128, 160, MODE>(p, ws, ws_floats, s);
+    return launch_tile<64, 160, MODE>(p, ws, ws_floats, s);
+  }
+  const int nt128 = ((p.M + 127) / 128) * ((p.N + 127) / 128);
+  if (nt128 >= 200 || p.M > 2048) return launch_tile<128, 128, MODE>(p, ws, ws_floats, s);
+  return launch_tile<64, 128, MODE>(p, ws, ws_floats, s);
+}
+
+// ---- elementwise helpers for the GEMM operands ------------------------------------------------------
+
+// GroupNorm apply (+SiLU): Y = act(X * scale[img, c] + shift[img, c]) on [nimg*HW, C] (16 B per thread)
+__global__ __launch_bounds__(256) void gn_apply_kernel(const half_t* __restrict__ X, long ldx, int HW, int C,
+                                                       const float* __restrict__ scale, const float* __restrict__ shift,
+                                                       int silu, half_t* __restrict__ Y, long ldy, long rows) {
+  const int cpr = C / 8;
+  const long n = rows * cpr;
+  for (long id = blockIdx.x * 256L + threadIdx.x; id < n; id += (long)gridDim.x * 256) {
+    const long r = id / cpr;
+    const int c = (int)(id - r * cpr) * 8;
+    const int img = (int)(r / HW);
+    half8 x = *reinterpret_cast<const half8*>(X + r * ldx + c);
+    const float* sc = scale + (long)img * C + c;
+    const float* sh = shift + (long)img * C + c;
+    float4v s0 = *reinterpret_cast<const float4v*>(sc), s1 = *reinterpret_cast<const float4v*>(sc + 4);
+    float4v h0 = *reinterpret_cast<const float4v*>(sh), h1 = *reinterpret_cast<const float4v*>(sh + 4);
+    float s[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+    float h[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+    half8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float f = (float)x[j] * s[j] + h[j];
+      if (silu) f = silu_f(f);
+      o[j] = (half_t)f;
+    }
+    *reinterpret_cast<half8*>(Y + r * ldy + c) = o;
+  }
+}
+
+// Wanda weight mask: Wm[n, k] = bit(n, k) ? 0 : W[n, k]   (bits [N][K/8], little-endian within a byte)
+__global__ __launch_bounds__(256) void mask_weight_kernel(const half_t* __restrict__ W, const uint8_t* __restrict__ bits,
+                                                          half_t* __restrict__ Wm, long n8) {
+  for (long id = blockIdx.x * 256L + threadIdx.x; id < n8; id += (long)gridDim.x * 256) {
+    half8 w = reinterpret_cast<const half8*>(W)[id];
+    const unsigned b = bits[id];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if ((b >> j) & 1u) w[j] = (half_t)0.f;
+    reinterpret_cast<half8*>(Wm)[id] = w;
+  }
+}
+
+int grid_for(long n) {
+  long g = (n + 255) / 256;
+  return (int)(g > 4096 ? 4096 : (g < 1 ? 1 : g));
 }
 
 }  // namespace
@@ -278,40 +391,69 @@ int dispatch(const GemmParams& p, hipStream_t s) {
 extern "C" int sdmoe_linear(const void* A, long lda, const void* W, long ldw, const void* bias,
                             const void* coladd, long coladd_bstride, int rows_per_batch,
                             const void* R, long ldr, void* C, long ldc, int M, int N, int K, int act,
-                            const float* a_scale, const float* a_shift, int a_silu,
-                            const void* wmask_bits, void* stream) {
+                            float* workspace, long workspace_floats, void* stream) {
   if (!A || !W || !C || M < 0 || N <= 0 || K <= 0) return SDMOE_EARG;
   if (M == 0) return SDMOE_OK;
   if (K % 64 || N % 8 || lda % 8 || ldw % 8 || ldc % 8 || (R && ldr % 8)) return SDMOE_ESHAPE;
-  if ((a_scale || coladd) && rows_per_batch <= 0) return SDMOE_EARG;
+  if (coladd && rows_per_batch <= 0) return SDMOE_EARG;
   GemmParams p{};
   p.A = (const half_t*)A; p.lda = lda; p.W = (const half_t*)W; p.ldw = ldw;
   p.bias = (const half_t*)bias; p.coladd = (const half_t*)coladd; p.coladd_bstride = coladd_bstride;
   p.R = (const half_t*)R; p.ldr = ldr; p.C = (half_t*)C; p.ldc = ldc;
   p.M = M; p.N = N; p.K = K; p.act = act;
-  p.a_scale = a_scale; p.a_shift = a_shift; p.a_silu = a_silu; p.a_chan = K;
   p.rows_per_batch = rows_per_batch > 0 ? rows_per_batch : 1;
-  p.wmask = (const uint8_t*)wmask_bits;
-  return dispatch<false>(p, (hipStream_t)stream);
+  const long ab = ((long)(M - 1) * lda + K) * 2, wb = ((long)(N - 1) * ldw + K) * 2;
+  if (ab >= (long)OOB || wb >= (long)OOB) return SDMOE_ESHAPE;
+  p.a_bytes = (int)ab; p.w_bytes = (int)wb;
+  return dispatch<MODE_GEMM>(p, workspace, workspace_floats, (hipStream_t)stream);
 }
 
 extern "C" int sdmoe_conv3x3(const void* X, long ldx, int nimg, int H, int W, int Cin,
                              const void* Wt, const void* bias, const void* coladd, long coladd_bstride,
                              const void* R, long ldr, void* Y, long ldy, int Cout, int stride, int upsample,
-                             int act, const float* a_scale, const float* a_shift, int a_silu, void* stream) {
+                             int act, float* workspace, long workspace_floats, void* stream) {
   if (!X || !Wt || !Y || nimg <= 0 || H <= 0 || W <= 0 || Cout <= 0) return SDMOE_EARG;
   if (Cin % 64 || Cout % 8 || ldx % 8 || ldy % 8 || (R && ldr % 8)) return SDMOE_ESHAPE;
   if (!(stride == 1 || stride == 2) || (upsample && stride != 1)) return SDMOE_EUNSUP;
   GemmParams p{};
   int OH, OW;
   if (upsample) { OH = 2 * H; OW = 2 * W; }
-  else { OH = (H + 2 - 3) / stride + 1; OW = (W + 2 - 3) / stride + 1; }
+  else { OH = (H - 1) / stride + 1; OW = (W - 1) / stride + 1; }
   p.A = (const half_t*)X; p.lda = ldx; p.W = (const half_t*)Wt; p.ldw = 9L * Cin;
   p.bias = (const half_t*)bias; p.coladd = (const half_t*)coladd; p.coladd_bstride = coladd_bstride;
   p.R = (const half_t*)R; p.ldr = ldr; p.C = (half_t*)Y; p.ldc = ldy;
   p.M = nimg * OH * OW; p.N = Cout; p.K = 9 * Cin; p.act = act;
-  p.a_scale = a_scale; p.a_shift = a_shift; p.a_silu = a_silu; p.a_chan = Cin;
   p.rows_per_batch = OH * OW;
   p.H = H; p.Wd = W; p.Cin = Cin; p.OH = OH; p.OW = OW; p.stride = stride; p.upsample = upsample;
-  return dispatch<true>(p, (hipStream_t)stream);
+  const long ab = ((long)nimg * H * W - 1) * ldx * 2 + (long)Cin * 2, wb = (long)Cout * 9 * Cin * 2;
+  if (ab >= (long)OOB || wb >= (long)OOB) return SDMOE_ESHAPE;
+  p.a_bytes = (int)ab; p.w_bytes = (int)wb;
+  if (upsample) return dispatch<MODE_CONV_UP>(p, workspace, workspace_floats, (hipStream_t)stream);
+  return dispatch<MODE_CONV>(p, workspace, workspace_floats, (hipStream_t)stream);
+}
+
+extern "C" int sdmoe_groupnorm_apply(const void* X, long ldx, int nimg, int HW, int C, const float* scale,
+                                     const float* shift, int silu, void* Y, long ldy, void* stream) {
+  if (!X || !Y || !scale || !shift || nimg <= 0 || HW <= 0 || C <= 0) return SDMOE_EARG;
+  if (C % 8 || ldx % 8 || ldy % 8) return SDMOE_ESHAPE;
+  const long rows = (long)nimg * HW;
+  gn_apply_kernel<<<grid_for(rows * (C / 8)), 256, 0, (hipStream_t)stream>>>(
+      (const half_t*)X, ldx, HW, C, scale, shift, silu, (half_t*)Y, ldy, rows);
+  SDMOE_CHECK_LAUNCH();
+  return SDMOE_OK;
+}
+
+extern "C" int sdmoe_mask_weight(const void* W, const void* bits, long N, long K, void* Wm, void* stream) {
+  if (!W || !bits || !Wm || N <= 0 || K <= 0) return SDMOE_EARG;
+  if (K % 8) return SDMOE_ESHAPE;
+  const long n8 = N * K / 8;
+  mask_weight_kernel<<<grid_for(n8), 256, 0, (hipStream_t)stream>>>((const half_t*)W, (const uint8_t*)bits,
+                                                                   (half_t*)Wm, n8);
+  SDMOE_CHECK_LAUNCH();
+  return SDMOE_OK;
+}
+
+extern "C" int sdmoe_tune(int knob, int value) {
+  if (knob == 0 && (value == 0 || value == 2 || value == 3)) { g_stages = value; return SDMOE_OK; }
+  return SDMOE_EARG;
 }

@@ -19,8 +19,10 @@ _FP = ctypes.POINTER(ctypes.c_float)
 
 # name -> argtypes, in the exact order of include/sdmoe.h
 SIGNATURES = {
-    "sdmoe_linear": [_P, _L, _P, _L, _P, _P, _L, _I, _P, _L, _P, _L, _I, _I, _I, _I, _P, _P, _I, _P, _P],
-    "sdmoe_conv3x3": [_P, _L, _I, _I, _I, _I, _P, _P, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _P, _P, _I, _P],
+    "sdmoe_linear": [_P, _L, _P, _L, _P, _P, _L, _I, _P, _L, _P, _L, _I, _I, _I, _I, _P, _L, _P],
+    "sdmoe_conv3x3": [_P, _L, _I, _I, _I, _I, _P, _P, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _P, _L, _P],
+    "sdmoe_groupnorm_apply": [_P, _L, _I, _I, _I, _P, _P, _I, _P, _L, _P],
+    "sdmoe_mask_weight": [_P, _P, _L, _L, _P, _P],
     "sdmoe_groupnorm_stats": [_P, _L, _I, _I, _I, _I, _P, _P, _F, _P, _P, _P, _L, _P],
     "sdmoe_layernorm": [_P, _L, _P, _L, _I, _I, _P, _P, _F, _P],
     "sdmoe_attention": [_P, _L, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _I, _F, _P],
@@ -29,6 +31,7 @@ SIGNATURES = {
     "sdmoe_prepare_input": [_P, _P, _I, _I, _L, _I, _P],
     "sdmoe_cfg_ddim_step": [_P, _L, _P, _I, _I, _I, _F, _F, _F, _P, _L, _P],
     "sdmoe_add": [_P, _P, _P, _L, _P],
+    "sdmoe_tune": [_I, _I],
     "sdmoe_version": [],
 }
 

@@ -48,11 +48,54 @@ def _dev(t: torch.Tensor, name: str, dtype=torch.float16):
     return t.data_ptr()
 
 
+_WS = {}
+WS_FLOATS = 32 * 1024 * 1024  # split-K fp32 partial slabs (128 MB per device), reused stream-ordered
+
+
+def _workspace(device):
+    ws = _WS.get(device)
+    if ws is None:
+        ws = _WS[device] = torch.empty(WS_FLOATS, dtype=torch.float32, device=device)
+    return ws
+
+
+def groupnorm_apply(x, nimg, HW, scale, shift, silu, out=None):
+    """out = (SiLU?)(x * scale[img, c] + shift[img, c]) on [nimg*HW, C] views."""
+    lib = _lib.load()
+    xp, ldx = _rows(x, "x")
+    C = x.shape[1]
+    if out is None:
+        out = torch.empty((x.shape[0], C), dtype=torch.float16, device=x.device)
+    op, ldy = _rows(out, "out")
+    st = lib.sdmoe_groupnorm_apply(xp, ldx, nimg, HW, C, scale.data_ptr(), shift.data_ptr(), int(bool(silu)), op,
+                                   ldy, _stream())
+    _lib.check(st, "sdmoe_groupnorm_apply")
+    return out
+
+
+def mask_weight(w, bits, out=None):
+    """Wanda-masked copy of w [N, K]: bit (n, k) of bits [N, K/8] set -> 0."""
+    lib = _lib.load()
+    N, K = w.shape
+    if tuple(bits.shape) != (N, K // 8) or bits.dtype != torch.uint8:
+        raise ValueError(f"mask bits {tuple(bits.shape)} {bits.dtype} do not match weight {tuple(w.shape)}")
+    if out is None:
+        out = torch.empty_like(w)
+    st = lib.sdmoe_mask_weight(_dev(w, "w"), _dev(bits, "bits", torch.uint8), N, K, _dev(out, "out"), _stream())
+    _lib.check(st, "sdmoe_mask_weight")
+    return out
+
+
 def linear(x, w, bias=None, *, out=None, residual=None, act=ACT_NONE, coladd=None, coladd_bstride=0,
            rows_per_batch=0, gn=None, wmask_bits=None):
     """out = act(GN?(x) @ w.T + bias + coladd) + residual.  w: [N, K] fp16 (nn.Linear layout).
-    gn = (scale, shift, silu) fp32 [images, K] per-(image, channel) GroupNorm apply fused into the load."""
+    gn = (scale, shift, silu): per-(image, channel) GroupNorm apply on x first (rows_per_batch rows/image).
+    wmask_bits: Wanda bitmask [N, K/8] zeroing weights (remove_wanda_neurons_fast.py:69-83)."""
     lib = _lib.load()
+    if gn is not None:
+        x = groupnorm_apply(x, x.shape[0] // rows_per_batch, rows_per_batch, gn[0], gn[1], gn[2])
+    if wmask_bits is not None:
+        w = mask_weight(w, wmask_bits)
     xp, lda = _rows(x, "x")
     M, K = x.shape
     N = w.shape[0]
@@ -63,20 +106,20 @@ def linear(x, w, bias=None, *, out=None, residual=None, act=ACT_NONE, coladd=Non
         out = torch.empty((M, N), dtype=torch.float16, device=x.device)
     op, ldc = _rows(out, "out")
     rp, ldr = (None, 0) if residual is None else _rows(residual, "residual")
-    sc = sh = None
-    silu = 0
-    if gn is not None:
-        sc, sh, silu = gn[0].data_ptr(), gn[1].data_ptr(), int(bool(gn[2]))
+    ws = _workspace(x.device)
     st = lib.sdmoe_linear(xp, lda, wp, w.stride(0), _ptr(bias), _ptr(coladd), coladd_bstride, rows_per_batch,
-                          rp, ldr, op, ldc, M, N, K, act, sc, sh, silu, _ptr(wmask_bits), _stream())
+                          rp, ldr, op, ldc, M, N, K, act, ws.data_ptr(), ws.numel(), _stream())
     _lib.check(st, "sdmoe_linear")
     return out
 
 
 def conv3x3(x, nimg, H, W, w, bias=None, *, stride=1, upsample=False, out=None, residual=None, act=ACT_NONE,
             coladd=None, coladd_bstride=0, gn=None):
-    """3x3 conv (pad 1) on NHWC x viewed as [nimg*H*W, Cin]; w: [Cout, 3, 3, Cin] fp16."""
+    """3x3 conv (pad 1) on NHWC x viewed as [nimg*H*W, Cin]; w: [Cout, 3, 3, Cin] fp16.
+    gn = (scale, shift, silu): GroupNorm(+SiLU) applied to x once (one read + write of x) before the conv."""
     lib = _lib.load()
+    if gn is not None:
+        x = groupnorm_apply(x, nimg, H * W, gn[0], gn[1], gn[2])
     xp, ldx = _rows(x, "x")
     Cin = x.shape[1]
     Cout = w.shape[0]
@@ -92,12 +135,9 @@ def conv3x3(x, nimg, H, W, w, bias=None, *, stride=1, upsample=False, out=None, 
         out = torch.empty((nimg * OH * OW, Cout), dtype=torch.float16, device=x.device)
     op, ldy = _rows(out, "out")
     rp, ldr = (None, 0) if residual is None else _rows(residual, "residual")
-    sc = sh = None
-    silu = 0
-    if gn is not None:
-        sc, sh, silu = gn[0].data_ptr(), gn[1].data_ptr(), int(bool(gn[2]))
+    ws = _workspace(x.device)
     st = lib.sdmoe_conv3x3(xp, ldx, nimg, H, W, Cin, _dev(w, "w"), _ptr(bias), _ptr(coladd), coladd_bstride, rp, ldr,
-                           op, ldy, Cout, stride, int(bool(upsample)), act, sc, sh, silu, _stream())
+                           op, ldy, Cout, stride, int(bool(upsample)), act, ws.data_ptr(), ws.numel(), _stream())
     _lib.check(st, "sdmoe_conv3x3")
     return out
 

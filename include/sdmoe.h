@@ -29,37 +29,42 @@ extern "C" {
 const char* sdmoe_version(void);
 
 /*
- * C[m, n] = act( sum_k A'[m, k] * W[n, k] + bias[n] + coladd[m / rows_per_batch][n] ) + R[m, n]
- * A' = A, or GroupNorm-applied A: A[m,k]*a_scale[img,k] + a_shift[img,k] (img = m / rows_per_batch), SiLU'd
- * when a_silu.  W is nn.Linear layout [N, K]; wmask_bits (optional) is a bitmask [N][K/8] bytes, bit j of byte
- * (n*K + k)/8 set => W[n, k] treated as 0.
+ * C[m, n] = act( sum_k A[m, k] * W[n, k] + bias[n] + coladd[m / rows_per_batch][n] ) + R[m, n]
+ * W is nn.Linear layout [N, K]. workspace (optional, fp32, workspace_floats elements) enables split-K for
+ * small tile grids; pass NULL/0 to disable.
  * Replaces: torch.nn.Linear / LoRACompatibleLinear.forward on the U-Net hot path (diffusers, external), the
  * GEGLU projection recomputed by MOEFy.hook_fn (neuron_receivers/moefy.py:12) and RemoveExperts.hook_fn
- * (neuron_receivers/remove_skilled_experts.py:26), and the masked down-projection
- * F.linear(x, W*(1-M), b) of WandaRemoveNeuronsFast.linear_hook_fn (neuron_receivers/remove_wanda_neurons_fast.py:69-83).
- * Requires K % 64 == 0, N % 8 == 0, strides % 8 == 0.
+ * (neuron_receivers/remove_skilled_experts.py:26), and F.linear(x, W*(1-M), b) of
+ * WandaRemoveNeuronsFast.linear_hook_fn (neuron_receivers/remove_wanda_neurons_fast.py:76, with
+ * sdmoe_mask_weight). Requires K % 64 == 0, N % 8 == 0, strides % 8 == 0.
  */
 int sdmoe_linear(const void* A, long lda, const void* W, long ldw, const void* bias, const void* coladd,
                  long coladd_bstride, int rows_per_batch, const void* R, long ldr, void* C, long ldc, int M, int N,
-                 int K, int act, const float* a_scale, const float* a_shift, int a_silu, const void* wmask_bits,
-                 void* stream);
+                 int K, int act, float* workspace, long workspace_floats, void* stream);
 
 /*
  * 3x3 convolution, padding 1, on NHWC X [nimg, H, W, Cin] (pixel stride ldx): stride 1 or 2, or a fused
  * nearest-neighbour 2x upsample in front (upsample=1, output 2H x 2W). Weights [Cout][3][3][Cin].
- * Same optional fusions as sdmoe_linear (GroupNorm+SiLU on the input, bias, per-image coladd (time
- * embedding), activation, residual R).
- * Replaces: diffusers ResnetBlock2D conv1/conv2 (+norm/SiLU/temb add/residual), Downsample2D, Upsample2D,
+ * Same fused epilogue as sdmoe_linear (bias, per-image coladd = time embedding, activation, residual R).
+ * Replaces: diffusers ResnetBlock2D conv1/conv2 (+temb add/residual), Downsample2D, Upsample2D,
  * conv_in/conv_out of UNet2DConditionModel (external). Requires Cin % 64 == 0, Cout % 8 == 0.
  */
 int sdmoe_conv3x3(const void* X, long ldx, int nimg, int H, int W, int Cin, const void* Wt, const void* bias,
                   const void* coladd, long coladd_bstride, const void* R, long ldr, void* Y, long ldy, int Cout,
-                  int stride, int upsample, int act, const float* a_scale, const float* a_shift, int a_silu,
-                  void* stream);
+                  int stride, int upsample, int act, float* workspace, long workspace_floats, void* stream);
+
+/* Y = (SiLU?)(X * scale[img, c] + shift[img, c]) on [nimg*HW, C] (the GroupNorm apply; scale/shift from
+ * sdmoe_groupnorm_stats). C % 8 == 0. */
+int sdmoe_groupnorm_apply(const void* X, long ldx, int nimg, int HW, int C, const float* scale, const float* shift,
+                          int silu, void* Y, long ldy, void* stream);
+
+/* Wm = W with every weight whose bit is set in bits [N][K/8] (little-endian bit order) zeroed: the device form
+ * of W * (1 - M) (remove_wanda_neurons_fast.py:75, 80). */
+int sdmoe_mask_weight(const void* W, const void* bits, long N, long K, void* Wm, void* stream);
 
 /*
  * GroupNorm statistics of X [nimg, HW, C] (row stride ldx) with `groups` groups: writes per (image, channel)
- * scale = rstd*gamma and shift = beta - mean*scale (fp32 [nimg, C]) consumed by the fused A-load above.
+ * scale = rstd*gamma and shift = beta - mean*scale (fp32 [nimg, C]) consumed by sdmoe_groupnorm_apply.
  * workspace: >= nimg*groups*64*2 floats.
  * Replaces: torch.nn.GroupNorm in ResnetBlock2D / Transformer2DModel / conv_norm_out (external).
  */
@@ -112,6 +117,9 @@ int sdmoe_prepare_input(const float* lat, void* out, int B, int HW, long ldo, in
  */
 int sdmoe_cfg_ddim_step(const void* eps, long lde, float* lat, int B, int HW, int do_cfg, float guidance,
                         float alpha_t, float alpha_prev, void* next_in, long ldn, void* stream);
+
+/* Tuning knobs for A/B experiments: knob 0 = GEMM LDS pipeline stages (2 or 3). */
+int sdmoe_tune(int knob, int value);
 
 /* out = a + b (fp16, n % 8 == 0). */
 int sdmoe_add(const void* a, const void* b, void* out, long n, void* stream);

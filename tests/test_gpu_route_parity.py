@@ -1,8 +1,11 @@
 """Parity of the HIP routing kernel and the receiver hooks against the REFERENCE's golden vectors (tests/golden).
 
 * route kernel fed the reference's own projection output y (fp16 cases): expert selection bit-exact on every
-  non-tie row, gated output bit-exact on those rows except where the device erf/GELU rounds a gate value to the
-  neighbouring fp16 (allowed: <= 1 fp16 ulp on < 0.1 % of elements);
+  row whose scores are identical and on every row whose k-th/(k+1)-th gap exceeds 2 fp16 ulps; gated output
+  bit-exact wherever the activated gate is. The activated gate itself may differ by a few fp16 ulps on a small
+  fraction of elements: the reference's CPU fp16 GELU is not correctly rounded (45 of 81,920 elements of one
+  fixture differ from the fp64-rounded value), and in the negative tail its fp32 1+erf(x/sqrt2) cancels
+  (our erfc form does not) -- measured max 3 ulps, 2 % of elements, in the gate-bias -1.5 fixture;
 * full hook (our proj GEMM + route) vs the reference hook: output within fp16 tolerance 2e-2 * max|ref|, and
   selection identical on rows whose k-th/(k+1)-th score gap exceeds the GEMM's fp16 rounding (near-ties counted).
 """
@@ -61,16 +64,17 @@ def near_tie_rows(score, k, slack_ulps=2):
 
 
 def check_out(o, ro, g, rg, h, rows):
-    """On `rows`: the activated gate equals the reference's up to one fp16 ulp (device vs host erf inside GELU;
-    < 0.2 % of elements differ at all), and the output is bit-identical wherever the gate is, otherwise within
-    |value| * ulp(gate) + ulp(out) (the product's exact propagation of that one-ulp gate difference)."""
+    """On `rows`: the activated gate equals the reference's up to 3 fp16 ulps (see module docstring; < 3 % of
+    elements differ at all), and the output is bit-identical wherever the gate is, otherwise within
+    |value| * |gate diff| + ulp(out) (the product's exact propagation of that gate difference)."""
     o, ro, g, rg, h = (a[rows].astype(np.float32) for a in (o, ro, g, rg, h))
     gd = np.abs(g - rg)
-    assert np.all(gd <= 1.01 * fp16_spacing(np.maximum(np.abs(g), np.abs(rg)))), f"gate max diff {gd.max()}"
-    assert (gd > 0).mean() < 2e-3, (gd > 0).mean()
+    sp = fp16_spacing(np.maximum(np.abs(g), np.abs(rg)))
+    assert np.all(gd <= 3.01 * sp), f"gate max ulps {(gd / sp).max()}"
+    assert (gd > 0).mean() < 3e-2, (gd > 0).mean()
     same = gd == 0
     assert np.array_equal(o[same], ro[same])
-    tol = np.abs(h) * fp16_spacing(np.maximum(np.abs(g), np.abs(rg))) + fp16_spacing(np.maximum(np.abs(o), np.abs(ro)))
+    tol = np.abs(h) * gd + fp16_spacing(np.maximum(np.abs(o), np.abs(ro)))
     assert np.all(np.abs(o - ro)[~same] <= 1.01 * tol[~same])
 
 

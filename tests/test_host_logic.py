@@ -1,0 +1,217 @@
+"""CPU-only tests of the host side: C-ABI library load + exported symbols, mask formats, receiver bookkeeping,
+scheduler constants, synthetic weights, routing layout. No GPU compute is launched here."""
+import ctypes
+import io
+import json
+import os
+import pickle
+import re
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    txt = open(os.path.join(ROOT, "include", "sdmoe.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(sdmoe_\w+)\(", txt, re.M)))
+
+
+def test_library_loads_and_exports_every_header_symbol():
+    from sdmoe import _lib
+    lib = _lib.load()
+    syms = header_symbols()
+    assert len(syms) >= 12
+    for s in syms:
+        assert hasattr(lib, s), f"{s} declared in include/sdmoe.h but not exported"
+        assert s in _lib.SIGNATURES, f"{s} has no ctypes signature"
+    assert set(_lib.SIGNATURES) == set(syms)
+    assert lib.sdmoe_version().decode().startswith("sdmoe-hip")
+
+
+def test_abi_argument_validation_without_gpu():
+    """Argument errors are reported as negative codes before anything is launched."""
+    from sdmoe import _lib
+    lib = _lib.load()
+    assert lib.sdmoe_linear(None, 0, None, 0, None, None, 0, 0, None, 0, None, 0, 1, 8, 64, 0, None, 0, None) == -1
+    assert lib.sdmoe_linear(1, 64, 1, 64, None, None, 0, 0, None, 0, 1, 8, 4, 8, 60, 0, None, 0, None) == -2
+    assert lib.sdmoe_conv3x3(1, 64, 1, 8, 8, 64, 1, None, None, 0, None, 0, 1, 8, 8, 3, 0, 0, None, 0, None) == -3
+    assert lib.sdmoe_attention(1, 8, 1, 8, 1, 8, 1, 8, 1, 4, 4, 1, 48, 1.0, None) == -3
+    assert lib.sdmoe_geglu_route(1, 8, 4, 16, 300, 4, 2, 1, 1, 1, None, 1, 16, None, 0, None, None, None) == -3
+    assert lib.sdmoe_geglu_route(1, 8, 4, 16, 8, 9, 2, 1, 1, 1, None, 1, 16, None, 0, None, None, None) == -1
+    assert lib.sdmoe_tune(0, 5) == -1 and lib.sdmoe_tune(0, 0) == 0
+
+
+def test_ops_refuse_cpu_tensors():
+    from sdmoe import ops, _lib
+    x = torch.zeros(4, 64, dtype=torch.float16)
+    with pytest.raises(_lib.SdmoeError):
+        ops.linear(x, torch.zeros(8, 64, dtype=torch.float16))
+
+
+def test_mask_pack_roundtrip_and_bit_order():
+    from sdmoe import mask_io
+    rng = np.random.default_rng(0)
+    m = (rng.random((320, 1280)) < 0.025).astype(np.int64)
+    bits = mask_io.pack_mask(m)
+    assert bits.shape == (320, 160) and bits.dtype == np.uint8
+    assert np.array_equal(mask_io.unpack_mask(bits, 1280), m)
+    # device contract: bit j of byte (n*K + k)/8 is element k = 8*byte + j (little bit order)
+    n, k = 7, 1000
+    m2 = np.zeros((320, 1280), dtype=np.int64)
+    m2[n, k] = 1
+    b2 = mask_io.pack_mask(m2).reshape(-1)
+    idx = (n * 1280 + k) // 8
+    assert b2[idx] == 1 << (k % 8) and b2.sum() == b2[idx]
+
+
+def test_restricted_unpickler_accepts_reference_formats_and_refuses_code(tmp_path):
+    import scipy.sparse
+    from sdmoe import mask_io
+    m = (np.random.default_rng(1).random((64, 256)) < 0.05).astype(np.int64)
+    p = tmp_path / "timestep_0_layer_0.pkl"
+    with open(p, "wb") as f:
+        pickle.dump(scipy.sparse.csr_matrix(m), f)  # modularity/wanda.py:169-173 format
+    assert np.array_equal(mask_io.load_mask_pickle(p), m)
+    p2 = tmp_path / "timestep_0_layer_1.pkl"
+    with open(p2, "wb") as f:
+        pickle.dump(np.asmatrix(m), f)  # benchmarks/save_union_experts.py:123-126 format
+    assert np.array_equal(mask_io.load_mask_pickle(p2), m)
+    p3 = tmp_path / "evil.pkl"
+    with open(p3, "wb") as f:
+        pickle.dump(os.system, f)
+    with pytest.raises(pickle.UnpicklingError):
+        mask_io.load_mask_pickle(p3)
+
+
+def test_wanda_masks_load_from_all_formats(tmp_path):
+    import scipy.sparse
+    from sdmoe import mask_io
+    from neuron_receivers import WandaRemoveNeuronsFast
+    rng = np.random.default_rng(2)
+    masks = [(rng.random((64, 256)) < 0.03).astype(np.int64) for _ in range(3)]
+    with open(tmp_path / "timestep_0_layer_0.pkl", "wb") as f:
+        pickle.dump(scipy.sparse.csr_matrix(masks[0]), f)
+    mask_io.save_wanda_mask(tmp_path, 0, 1, masks[1])
+    idx = np.argwhere(masks[2]).tolist()
+    json.dump(idx, open(tmp_path / "timestep_0_layer_2.json", "w"))
+    rec = WandaRemoveNeuronsFast(0, str(tmp_path), 1, 3, weights_shape=[(64, 256)] * 3)
+    for l in range(3):
+        assert np.array_equal(rec.dense_mask(0, l), masks[l])
+
+
+def test_union_of_packed_masks_equals_oracle_or():
+    from oracle import hooks_ref as H
+    from sdmoe import mask_io
+    from neuron_receivers import WandaRemoveNeuronsFast, MultiConceptRemoverWanda
+    rng = np.random.default_rng(3)
+    T, L = 2, 2
+    concepts = {c: {t: {l: (rng.random((32, 128)) < 0.05).astype(np.int64) for l in range(L)} for t in range(T)}
+                for c in ("a", "b", "c")}
+    removers = {c: WandaRemoveNeuronsFast(0, None, T, L, masks=m) for c, m in concepts.items()}
+    mc = MultiConceptRemoverWanda(None, 0, T, L, concepts_to_remove=list(concepts), removers=removers)
+    mc.handle_multiple_concepts(["a", "c"])
+    for t in range(T):
+        for l in range(L):
+            exp = H.union_masks([concepts["a"][t][l], concepts["c"][t][l]])
+            assert np.array_equal(mc.union_neuron_remover.dense_mask(t, l), exp)
+    mc.reset_union_remover()
+    assert mc.union_neuron_remover.dense_mask(0, 0).sum() == 0
+
+
+def test_union_random_drop_is_seeded_and_subset():
+    from oracle import hooks_ref as H
+    rng = np.random.default_rng(4)
+    ms = [(rng.random((40, 80)) < 0.1).astype(np.int64) for _ in range(4)]
+    u1 = H.union_with_random_drop(ms, 0.95, seed=7)
+    u2 = H.union_with_random_drop(ms, 0.95, seed=7)
+    assert np.array_equal(u1, u2)
+    full = H.union_masks(ms)
+    assert np.all(u1 <= full) and u1.sum() < full.sum()
+
+
+def test_counter_semantics_match_reference_receivers():
+    from neuron_receivers import NeuronPredictivity
+    from oracle.hooks_ref import TimeLayerCounter
+    r = NeuronPredictivity(0, 51, 16)
+    o = TimeLayerCounter(16)
+    for _ in range(16 * 51 + 5):
+        assert (r.timestep, r.layer) == (o.timestep, o.layer)
+        r.update_time_layer()
+        o.update()
+    r.reset_time_layer()
+    assert (r.timestep, r.layer) == (0, 0)
+
+
+def test_remove_experts_constructor_fixes_snapshot_defects(tmp_path):
+    """App. A #1/#2: replace_fn is accepted as a keyword; keep_nsfw does not land in replace_fn."""
+    from neuron_receivers import GEGLU, RemoveExperts
+    for t in range(2):
+        for l in range(2):
+            json.dump([t, l], open(tmp_path / f"timestep_{t}_layer_{l}.json", "w"))
+    r = RemoveExperts(0, str(tmp_path), 2, 2, keep_nsfw=True, replace_fn=GEGLU)
+    assert r.replace_fn is GEGLU and r.keep_nsfw is True
+    assert r.expert_indices[1][0] == [1, 0]
+
+
+def test_ddim_schedule_matches_oracle():
+    from sdmoe.pipeline import ddim_schedule
+    from oracle.unet_ref import ddim_schedule as ref
+    ts, at, ap = ddim_schedule(50)
+    rts, rat, rap = ref(50)
+    assert list(ts) == list(rts) and ts[0] == 981 and ts[-1] == 1
+    assert np.allclose(at, rat, rtol=0, atol=0) and np.allclose(ap, rap, rtol=0, atol=0)
+
+
+def test_synthetic_weights_match_sd14_architecture():
+    import math
+    from sdmoe.config import UNetConfig
+    from sdmoe.weights import param_specs, make_state_dict
+    cfg = UNetConfig.sd14()
+    specs = param_specs(cfg)
+    assert sum(math.prod(s) for _, s, _ in specs) == 859_520_964  # SD-1.4 UNet2DConditionModel
+    geglu = [n for n, _, _ in specs if n.endswith("ff.net.0.proj.weight")]
+    assert len(geglu) == 16
+    assert [n[:-len(".proj.weight")] for n in sorted(geglu)] == [n for n, _ in cfg.geglu_layers()]
+    sd1 = make_state_dict(cfg, 0, names={"conv_in.weight", "mid_block.resnets.0.conv1.bias"})
+    sd2 = make_state_dict(cfg, 0, names={"conv_in.weight"})
+    assert torch.equal(sd1["conv_in.weight"], sd2["conv_in.weight"])
+
+
+def test_routing_layout_from_patterns():
+    from sdmoe.ops import Routing
+    from oracle.hooks_ref import patterns_from_labels
+    from moefication.helper import balanced_random_labels
+    lab = balanced_random_labels(1280, 20, 0)
+    P = patterns_from_labels(lab)
+    r = Routing.from_patterns(P, 12, "cpu")
+    assert r.E == 64 and r.k == 12 and r.F == 1280
+    off = r.e_off.numpy()
+    nid = r.e_nid.numpy()
+    for e in (0, 17, 63):
+        members = nid[off[e]:off[e + 1]]
+        assert len(members) == 20 and np.all(lab[members] == e) and np.all(np.diff(members) > 0)
+    with pytest.raises(ValueError):
+        Routing.from_patterns(torch.ones(2, 4), 1, "cpu")
+
+
+def test_removed_bits_packing():
+    from sdmoe.ops import removed_bits
+    b = removed_bits([0, 31, 32, 255], 256, "cpu").numpy().view(np.uint32)
+    assert b.shape == (8,) and b[0] == (1 | (1 << 31)) and b[1] == 1 and b[7] == 1 << 31
+    with pytest.raises(IndexError):
+        removed_bits([256], 256, "cpu")
+
+
+def test_modify_ffn_reads_reference_label_format(tmp_path):
+    """moe_utils.py:54-61 writes torch.save(list[int]); helper.modify_ffn sets patterns [E, 4C] and k."""
+    from moefication.helper import modify_ffn, balanced_random_labels
+    from sdmoe.unet import GEGLU, LoRACompatibleLinear
+    g = GEGLU(LoRACompatibleLinear(torch.zeros(2 * 1280, 320, dtype=torch.float16)))
+    lab = balanced_random_labels(1280, 20, 1)
+    torch.save([int(v) for v in lab], tmp_path / "labels")
+    modify_ffn(g, str(tmp_path / "labels"), 0.2)
+    assert tuple(g.patterns.shape) == (64, 1280) and g.k == 12 and g.patterns.dtype == torch.float16
+    assert torch.equal(g.patterns.float().argmax(0), torch.from_numpy(lab))

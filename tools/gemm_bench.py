@@ -1,0 +1,75 @@
+"""Microbenchmark of the sdmoe GEMM / conv / attention kernels on the U-Net's real shapes (nimg = 2*B images).
+usage: python tools/gemm_bench.py [--nimg 16] [--iters 20]"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "diffusion-models-moe_amd"), ROOT]
+
+import torch  # noqa: E402
+
+from sdmoe import ops  # noqa: E402
+
+
+def timeit(fn, iters):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--nimg", type=int, default=16)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--stages", type=int, default=0)
+    a = ap.parse_args()
+    from sdmoe import _lib
+    _lib.check(_lib.load().sdmoe_tune(0, a.stages), "tune")
+    print("stages", a.stages)
+    n = a.nimg
+    dev = "cuda"
+    rows = []
+    # convs: (H, Cin, Cout, stride, upsample)
+    for H, Cin, Cout, st, up in [(64, 320, 320, 1, 0), (64, 640, 320, 1, 0), (32, 640, 640, 1, 0),
+                                  (32, 1280, 640, 1, 0), (16, 1280, 1280, 1, 0), (16, 2560, 1280, 1, 0),
+                                  (8, 1280, 1280, 1, 0), (8, 2560, 1280, 1, 0), (64, 320, 320, 2, 0),
+                                  (32, 640, 640, 1, 1), (64, 320, 8, 1, 0)]:
+        x = torch.randn(n * H * H, Cin, device=dev).half()
+        w = (torch.randn(Cout, 3, 3, Cin, device=dev) * (9 * Cin) ** -0.5).half()
+        b = torch.zeros(Cout, device=dev).half()
+        OH = 2 * H if up else (H - 1) // st + 1
+        ms = timeit(lambda: ops.conv3x3(x, n, H, H, w, b, stride=st, upsample=bool(up)), a.iters)
+        fl = 2.0 * n * OH * OH * Cout * 9 * Cin
+        rows.append((f"conv {H}x{H} {Cin}->{Cout} s{st}{' up' if up else ''}", ms, fl / ms / 1e9))
+    # linears: (M, N, K)
+    for M, N, K in [(n * 4096, 960, 320), (n * 4096, 2560, 320), (n * 4096, 320, 1280), (n * 4096, 320, 320),
+                    (n * 1024, 5120, 640), (n * 1024, 640, 2560), (n * 256, 10240, 1280), (n * 256, 1280, 5120),
+                    (n * 64, 3840, 1280), (n * 77, 2560, 768)]:
+        x = torch.randn(M, K, device=dev).half()
+        w = (torch.randn(N, K, device=dev) * K ** -0.5).half()
+        ms = timeit(lambda: ops.linear(x, w), a.iters)
+        rows.append((f"linear M={M} N={N} K={K}", ms, 2.0 * M * N * K / ms / 1e9))
+    for N_, d, Nk in [(4096, 40, 4096), (4096, 40, 77), (1024, 80, 1024), (256, 160, 256)]:
+        C = 8 * d
+        q = torch.randn(n * N_, 3 * C, device=dev).half()
+        kv = torch.randn(n * Nk, 2 * C, device=dev).half()
+        if Nk == N_:
+            f = lambda: ops.attention(q[:, :C], q[:, C:2 * C], q[:, 2 * C:], n, N_, Nk, 8)  # noqa: E731
+        else:
+            f = lambda: ops.attention(q[:, :C], kv[:, :C], kv[:, C:], n, N_, Nk, 8)  # noqa: E731
+        ms = timeit(f, a.iters)
+        rows.append((f"attn N={N_} d={d} Nk={Nk}", ms, 4.0 * n * 8 * N_ * Nk * d / ms / 1e9))
+    for name, ms, tf in rows:
+        print(f"{name:42s} {ms*1e3:9.1f} us {tf:8.1f} TF/s")
+
+
+if __name__ == "__main__":
+    main()

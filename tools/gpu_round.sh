@@ -1,5 +1,6 @@
+set -u
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -q -m gpu -p no:cacheprovider > gpurun_out/t2.log 2>&1; echo "pytest exit $?"
-tail -30 gpurun_out/t2.log
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke2.log 2>&1; echo "smoke exit $?"; tail -5 gpurun_out/smoke2.log
-timeout -k 10 600 python bench.py --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/bench2.log 2>&1; echo "bench exit $?"; tail -5 gpurun_out/bench2.log
+timeout -k 10 900 python -m pytest tests -q -m gpu -p no:cacheprovider > gpurun_out/t6.log 2>&1; echo "pytest exit $?"; tail -12 gpurun_out/t6.log
+timeout -k 10 600 python bench.py --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/bench6.log 2>&1; echo "bench exit $?"; tail -1 gpurun_out/bench6.log
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof6 -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 1 --inference-steps 10 --no-cpu-baseline --no-roofline > $GRAFT_REPO_ROOT/gpurun_out/bench6p.log 2>&1; echo "prof exit $?"
