@@ -44,6 +44,8 @@ __global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn_fwd_kernel(AttnP
   constexpr int CH = D / 8;                   // 16-B chunks per row
   constexpr int TOT = KB * CH;
   constexpr int PER = (TOT + 255) / 256;
+  constexpr bool SUM_BY_MFMA = DV > D;     // V column D = 1.0 -> O^T row D accumulates sum_k P[k][q]
+  constexpr float RESCALE_THR = 8.0f;
 
   __shared__ __attribute__((aligned(16))) half_t Ks[KB * KS];
   __shared__ __attribute__((aligned(16))) half_t Vs[KB * VS];
@@ -64,7 +66,7 @@ __global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn_fwd_kernel(AttnP
   }
   for (int i = tid; i < KB * (VS - D); i += 256) {
     int r = i / (VS - D), c = D + i % (VS - D);
-    Vs[r * VS + c] = (half_t)0.f;
+    Vs[r * VS + c] = (half_t)((SUM_BY_MFMA && c == D) ? 1.f : 0.f);
   }
 
   // Q fragments (B operand of S^T = K Q^T): lane holds Q[q = w][d = 32c + 8g + j]
@@ -142,39 +144,50 @@ __global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn_fwd_kernel(AttnP
         for (int f = 0; f < 2; ++f) s[f][kf] = mfma16x16x32(a, qf[f][c], s[f][kf]);
       }
 
-    // ---- online softmax (query on the lane)
+    // ---- online softmax (query on the lane), VALU-lean:
+    //  * raw-score max (scale > 0 commutes with max), scale folded into the exp2 argument: p = 2^(s*c - m);
+    //  * key masking only on the ragged last tile (uniform branch);
+    //  * deferred rescale: the running max moves only when some query's tile max exceeds it by > RESCALE_THR
+    //    (log2 units), so most tiles skip the O/l rescale; p <= 2^RESCALE_THR stays well inside fp16;
+    //  * for D with a pad column (D = 40) the row sum comes out of the PV MFMA (V pad column = 1.0).
     const int kbase = kt * KB;
+    const bool ragged = kbase + KB > p.Nk;
     half8 pb[2][2];
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
-      float mx = -1e30f;
+      if (ragged) {
 #pragma unroll
-      for (int kf = 0; kf < 4; ++kf)
+        for (int kf = 0; kf < 4; ++kf)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int key = kbase + kf * 16 + 4 * g + i;
-          float v = s[f][kf][i] * p.scale_log2;
-          v = key < p.Nk ? v : -INFINITY;
-          s[f][kf][i] = v;
-          mx = fmaxf(mx, v);
-        }
+          for (int i = 0; i < 4; ++i)
+            if (kbase + kf * 16 + 4 * g + i >= p.Nk) s[f][kf][i] = -INFINITY;
+      }
+      float mx = fmaxf(fmaxf(s[f][0][0], s[f][0][1]), fmaxf(s[f][0][2], s[f][0][3]));
+#pragma unroll
+      for (int kf = 1; kf < 4; ++kf)
+        mx = fmaxf(mx, fmaxf(fmaxf(s[f][kf][0], s[f][kf][1]), fmaxf(s[f][kf][2], s[f][kf][3])));
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(mrun[f], mx);
-      const float alpha = exp2f(mrun[f] - mnew);
-      mrun[f] = mnew;
+      const float mxs = mx * p.scale_log2;
+      if (!__all(mxs - mrun[f] <= RESCALE_THR)) {  // wave-uniform decision
+        const float mnew = fmaxf(mrun[f], mxs);
+        const float alpha = __builtin_amdgcn_exp2f(mrun[f] - mnew);
+        mrun[f] = mnew;
+        if (!SUM_BY_MFMA) lrun[f] *= alpha;
+#pragma unroll
+        for (int d = 0; d < NDF; ++d) oacc[f][d] *= alpha;
+      }
+      const float nm = -mrun[f];
       float ls = 0.f;
 #pragma unroll
       for (int kf = 0; kf < 4; ++kf)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float e = exp2f(s[f][kf][i] - mnew);
+          const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(s[f][kf][i], p.scale_log2, nm));
           s[f][kf][i] = e;
-          ls += e;
+          if (!SUM_BY_MFMA) ls += e;
         }
-      lrun[f] = lrun[f] * alpha + ls;
-#pragma unroll
-      for (int d = 0; d < NDF; ++d) oacc[f][d] *= alpha;
+      if (!SUM_BY_MFMA) lrun[f] += ls;
 #pragma unroll
       for (int c2 = 0; c2 < 2; ++c2) {
         half8 v;
@@ -209,9 +222,15 @@ __global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn_fwd_kernel(AttnP
   half_t* Ob = p.O + (long)b * p.Nq * p.ldo + h * D;
 #pragma unroll
   for (int f = 0; f < 2; ++f) {
-    float l = lrun[f];
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
+    float l;
+    if (SUM_BY_MFMA) {
+      // O^T row D (df = D/16, lane group g = (D%16)/4, register D%4) holds sum_k P[k][q]; broadcast to all g
+      l = __shfl(oacc[f][D / 16][D % 4], ((D % 16) / 4) * 16 + w, 64);
+    } else {
+      l = lrun[f];
+      l += __shfl_xor(l, 16, 64);
+      l += __shfl_xor(l, 32, 64);
+    }
     const float inv = 1.0f / l;
     const int q = q0 + f * 16 + w;
     if (q >= p.Nq) continue;

@@ -1,8 +1,8 @@
 // Normalisation kernels for the SD U-Net step (gfx950).
 //
-// GroupNorm is split into a statistics pass and an APPLY that is fused into the consumer's A-operand load
-// (gemm.hip): the stats pass reads the activation once and emits per-(image, channel) fp32 scale/shift,
-// so GN(+SiLU) never writes a normalised copy of the activation to HBM.
+// GroupNorm is split into a statistics pass (this file: one coalesced read of the activation -> per-(image,
+// channel) fp32 scale/shift) and a vectorised apply(+SiLU) pass (gemm.hip, sdmoe_groupnorm_apply) that feeds
+// the LDS-DMA conv/GEMM. (Applying it inside the conv's operand load would redo it for all 9 taps x N-tiles.)
 //   diffusers ResnetBlock2D norm1/norm2 (GroupNorm(32, C, eps=1e-5)), Transformer2DModel.norm
 //   (GroupNorm(32, C, eps=1e-6)), conv_norm_out.
 // LayerNorm (BasicTransformerBlock norm1/2/3, eps=1e-5) is one wave per token row, two-pass in registers.
@@ -11,33 +11,60 @@
 
 namespace {
 
-// Partial sums of (x - ref) and (x - ref)^2 over a slice of rows for one (image, group).
+// Partial sums of (x - ref) and (x - ref)^2 over a slice of rows of one image, for every group at once.
 // ref = first element of the group in the image's row 0 (shifted sums keep the variance well conditioned).
+// Reads whole rows with 16-B loads: "virtual thread" vt (NV per thread) owns 8-channel chunk vt % nch and row
+// phase vt / nch, accumulates per-channel sums in registers; LDS reduces phases, then channels per group.
+template <int NV>
 __global__ __launch_bounds__(256) void gn_partial_kernel(const half_t* __restrict__ X, long ldx, int HW, int C,
                                                          int G, int S, float2* __restrict__ part) {
-  const int s = blockIdx.x, g = blockIdx.y, img = blockIdx.z;
-  const int cpg = C / G, hp = cpg / 2;
+  __shared__ float red[256 * NV][17];
+  __shared__ float csum[2][2560];
+  __shared__ float refs[64];
+  const int s = blockIdx.x, img = blockIdx.y, tid = threadIdx.x;
+  const int cpg = C / G, nch = C / 8;
+  const int RP = max(1, (256 * NV) / nch);
   const int r0 = (int)((long)HW * s / S), r1 = (int)((long)HW * (s + 1) / S);
-  const half_t* base = X + (long)img * HW * ldx + g * cpg;
-  const float ref = (float)base[0];
-  float s1 = 0.f, s2 = 0.f;
-  const int n = (r1 - r0) * hp;
-  for (int e = threadIdx.x; e < n; e += 256) {
-    const int r = r0 + e / hp, pr = e % hp;
-    half2_t v = *reinterpret_cast<const half2_t*>(base + (long)r * ldx + 2 * pr);
-    const float a = (float)v[0] - ref, b = (float)v[1] - ref;
-    s1 += a + b;
-    s2 += a * a + b * b;
-  }
-  s1 = wave_sum(s1);
-  s2 = wave_sum(s2);
-  __shared__ float r[2][4];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) { r[0][wave] = s1; r[1][wave] = s2; }
+  const half_t* base = X + (long)img * HW * ldx;
+  if (tid < G) refs[tid] = (float)base[tid * cpg];
   __syncthreads();
-  if (threadIdx.x == 0) {
-    part[((long)img * G + g) * S + s] = make_float2(r[0][0] + r[0][1] + r[0][2] + r[0][3],
-                                                    r[1][0] + r[1][1] + r[1][2] + r[1][3]);
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int vt = tid + 256 * j;
+    if (vt < nch * RP) {
+      const int c = vt % nch, ph = vt / nch;
+      float rf[8], s1[8], s2[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { rf[i] = refs[(c * 8 + i) / cpg]; s1[i] = 0.f; s2[i] = 0.f; }
+      for (int r = r0 + ph; r < r1; r += RP) {
+        half8 v = *reinterpret_cast<const half8*>(base + (long)r * ldx + c * 8);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float a = (float)v[i] - rf[i];
+          s1[i] += a;
+          s2[i] = __builtin_fmaf(a, a, s2[i]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { red[vt][i] = s1[i]; red[vt][8 + i] = s2[i]; }
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < nch; c += 256) {
+    float a[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) a[i] = 0.f;
+    for (int ph = 0; ph < RP; ++ph)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) a[i] += red[ph * nch + c][i];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { csum[0][c * 8 + i] = a[i]; csum[1][c * 8 + i] = a[8 + i]; }
+  }
+  __syncthreads();
+  if (tid < G) {
+    float a = 0.f, b = 0.f;
+    for (int c = tid * cpg; c < (tid + 1) * cpg; ++c) { a += csum[0][c]; b += csum[1][c]; }
+    part[((long)img * G + tid) * S + s] = make_float2(a, b);
   }
 }
 
@@ -123,15 +150,19 @@ extern "C" int sdmoe_groupnorm_stats(const void* X, long ldx, int nimg, int HW, 
                                      float* workspace, long workspace_floats, void* stream) {
   if (!X || !gamma || !beta || !scale || !shift || !workspace || nimg <= 0 || HW <= 0 || groups <= 0)
     return SDMOE_EARG;
-  if (C % groups || (C / groups) % 2 || ldx % 2) return SDMOE_ESHAPE;
-  const long elems = (long)HW * (C / groups);
-  int S = (int)(elems / 8192);
-  S = S < 1 ? 1 : (S > 64 ? 64 : S);
-  if (S > HW) S = HW;
+  if (C % groups || C % 8 || ldx % 8 || C > 2560 || groups > 64) return SDMOE_ESHAPE;
+  // ~1024 workgroups in total, every slice at least 8 rows
+  int S = (1024 + nimg - 1) / nimg;
+  if (S > HW / 8) S = HW / 8;
+  if (S > 64) S = 64;
+  if (S < 1) S = 1;
   if ((long)nimg * groups * S * 2 > workspace_floats) return SDMOE_EARG;
   hipStream_t s = (hipStream_t)stream;
   float2* part = reinterpret_cast<float2*>(workspace);
-  gn_partial_kernel<<<dim3(S, groups, nimg), 256, 0, s>>>((const half_t*)X, ldx, HW, C, groups, S, part);
+  if (C / 8 > 256)
+    gn_partial_kernel<2><<<dim3(S, nimg), 256, 0, s>>>((const half_t*)X, ldx, HW, C, groups, S, part);
+  else
+    gn_partial_kernel<1><<<dim3(S, nimg), 256, 0, s>>>((const half_t*)X, ldx, HW, C, groups, S, part);
   SDMOE_CHECK_LAUNCH();
   gn_finalize_kernel<<<dim3(groups, nimg), 64, 0, s>>>((const half_t*)X, ldx, HW, C, groups, S, part,
                                                        (const half_t*)gamma, (const half_t*)beta, eps, scale, shift);

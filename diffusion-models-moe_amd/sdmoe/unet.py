@@ -10,8 +10,8 @@ Everything else is MI355X-first:
   * activations live in HBM as NHWC fp16 [images*H*W, C] (the transformer's token layout, so no permutes);
   * skip concatenations are zero-copy: each up-block ResNet input is one [rows, C_prev + C_skip] buffer; the
     down path writes its skip outputs straight into the right-hand channel slice and reads them from there;
-  * GroupNorm(+SiLU) is applied inside the consuming conv/GEMM's operand load (stats pass only), the time
-    embedding add, bias, residual adds and activations are GEMM/conv epilogues;
+  * GroupNorm is one coalesced statistics pass + one vectorised apply(+SiLU) pass feeding the LDS-DMA
+    conv/GEMM; the time-embedding add, bias, residual adds and activations are GEMM/conv epilogues;
   * attention projections are fused (QKV [3C, C], cross KV [2C, 768]) and attention reads the heads in place;
   * all 22 ResNet time-embedding projections run as ONE GEMM per step.
 """
@@ -134,13 +134,14 @@ class GEGLU(nn.Module):
             self._routing_key = key
         return self._routing
 
-    def routed(self, x, removed=None, want_gate=False):
-        """proj GEMM + routed GEGLU kernel. x: [..., C] fp16. Returns (out [..., 4C], masked gate or None)."""
+    def routed(self, x, removed=None, want_gate=False, sel_out=None):
+        """proj GEMM + routed GEGLU kernel. x: [..., C] fp16. Returns (out [..., 4C], masked gate or None).
+        sel_out (optional int32 [tokens, ceil(E/32)]) receives the per-token top-k expert bitmask."""
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
         y = self.proj.run(x2)
         gate = torch.empty((x2.shape[0], self.inner_dim), dtype=torch.float16, device=x.device) if want_gate else None
-        out = ops.geglu_route(y, self.routing(), act_code(self.gelu), removed=removed, gate_out=gate)
+        out = ops.geglu_route(y, self.routing(), act_code(self.gelu), removed=removed, gate_out=gate, sel_out=sel_out)
         out = out.view(*shp[:-1], self.inner_dim)
         return out, (gate.view(*shp[:-1], self.inner_dim) if want_gate else None)
 
