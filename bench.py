@@ -43,7 +43,8 @@ def parse():
     p.add_argument("--no-roofline", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-evals", type=int, default=2, help="CPU oracle U-Net evaluations to time")
-    p.add_argument("--traffic", type=str, default=None, help="PMC summary json from tools/pmc_traffic.py")
+    p.add_argument("--traffic", type=str, default=os.path.join(ROOT, "profiles", "pmc_conv_traffic.json"),
+                   help="PMC summary json from tools/pmc_traffic.py (HBM bytes per conv launch)")
     return p.parse_args()
 
 
@@ -150,12 +151,13 @@ class KernelTimer:
             setattr(U.ops, self.family, wrapped)
 
     def account(self, a, k, out):
-        x, w = a[0], a[4]
-        cin_real = 4 if getattr(w, "_sdmoe_conv_in", False) else x.shape[1]  # conv_in: 4 real of 64 padded
+        # conv3x3_launch(xp, ldx, nimg, H, W, Cin, w, ...): algorithmic FLOPs = 2 * M * Cout * 9 * Cin (real
+        # channel counts: conv_in has 4 of its 64 padded input channels, conv_out 4 of its 8 padded outputs)
+        w = a[6]
+        cin_real = 4 if getattr(w, "_sdmoe_conv_in", False) else a[5]
         M = out.shape[0]
-        N = 4 if getattr(w, "_sdmoe_conv_out", False) else w.shape[0]  # conv_out: 4 real of 8 padded
+        N = 4 if getattr(w, "_sdmoe_conv_out", False) else w.shape[0]
         self.flops += 2.0 * M * N * 9 * cin_real
-        self.bytes += (x.shape[0] * x.shape[1] + w.numel() + out.numel()) * 2.0
 
     def result(self):
         torch.cuda.synchronize()
@@ -218,7 +220,7 @@ def main():
     prompts = [f"synthetic prompt {i}" for i in range(world * args.batch)]
     mine, offset = D.shard(prompts, rank, world)
 
-    timer = KernelTimer("conv3x3")
+    timer = KernelTimer("conv3x3_launch")
     if not args.no_roofline:
         timer.wrap(ops)
     pipe.unet.conv_in.weight._sdmoe_conv_in = True
@@ -269,7 +271,8 @@ def main():
             traffic = None
             if args.traffic and os.path.exists(args.traffic):
                 traffic = json.load(open(args.traffic)).get("bytes_per_launch")
-            roof = {"bound": "mfma", "kernel": "sdmoe conv3x3 implicit-GEMM (gemm_kernel<...,CONV=true,...>)",
+            roof = {"bound": "mfma", "kernel": "sdmoe_conv3x3: implicit-GEMM conv (gemm_kernel<BM,BN,MODE=1|2,STAGES>"
+                                               " + split-K reduce where used)",
                     "achieved": round(achieved, 1), "peak": PEAK_FP16_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(achieved / PEAK_FP16_TFLOPS, 4), "traffic": traffic,
                     "launches": n, "avg_launch_ms": round(ms / n, 4),

@@ -135,7 +135,15 @@ def conv3x3(x, nimg, H, W, w, bias=None, *, stride=1, upsample=False, out=None, 
         out = torch.empty((nimg * OH * OW, Cout), dtype=torch.float16, device=x.device)
     op, ldy = _rows(out, "out")
     rp, ldr = (None, 0) if residual is None else _rows(residual, "residual")
-    ws = _workspace(x.device)
+    return conv3x3_launch(xp, ldx, nimg, H, W, Cin, w, bias, coladd, coladd_bstride, rp, ldr, out, op, ldy, Cout,
+                          stride, upsample, act)
+
+
+def conv3x3_launch(xp, ldx, nimg, H, W, Cin, w, bias, coladd, coladd_bstride, rp, ldr, out, op, ldy, Cout, stride,
+                   upsample, act):
+    """The sdmoe_conv3x3 launch alone (bench.py times exactly this with HIP events)."""
+    lib = _lib.load()
+    ws = _workspace(out.device)
     st = lib.sdmoe_conv3x3(xp, ldx, nimg, H, W, Cin, _dev(w, "w"), _ptr(bias), _ptr(coladd), coladd_bstride, rp, ldr,
                            op, ldy, Cout, stride, int(bool(upsample)), act, ws.data_ptr(), ws.numel(), _stream())
     _lib.check(st, "sdmoe_conv3x3")

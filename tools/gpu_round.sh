@@ -1,7 +1,9 @@
 set -u
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -q -m gpu -p no:cacheprovider > gpurun_out/t7.log 2>&1; echo "pytest exit $?"; tail -8 gpurun_out/t7.log
-timeout -k 10 300 python tools/gemm_bench.py > gpurun_out/gb7.log 2>&1; echo "gemm_bench exit $?"; grep attn gpurun_out/gb7.log
-timeout -k 10 600 python bench.py --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/bench7.log 2>&1; echo "bench exit $?"; tail -1 gpurun_out/bench7.log | cut -c1-400
+R=$GRAFT_REPO_ROOT
+timeout -k 10 900 python bench.py > gpurun_out/bench8.log 2>&1; echo "bench exit $?"; tail -1 gpurun_out/bench8.log
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof7 -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 1 --inference-steps 10 --no-cpu-baseline --no-roofline > $GRAFT_REPO_ROOT/gpurun_out/bench7p.log 2>&1; echo "prof exit $?"
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof8 -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline > $R/gpurun_out/bench8p.log 2>&1; echo "prof exit $?"; tail -1 $R/gpurun_out/bench8p.log | cut -c1-300
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/pmc8f -o run --output-format csv -- python3 $R/bench.py --inference-steps 2 --steps 1 --warmup 0 --no-cpu-baseline --no-roofline > $R/gpurun_out/pmc8f.log 2>&1; echo "pmc fetch exit $?"
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/pmc8w -o run --output-format csv -- python3 $R/bench.py --inference-steps 2 --steps 1 --warmup 0 --no-cpu-baseline --no-roofline > $R/gpurun_out/pmc8w.log 2>&1; echo "pmc write exit $?"
+ls $R/gpurun_out/pmc8f $R/gpurun_out/pmc8w

@@ -1,0 +1,64 @@
+"""HBM traffic per launch of a kernel family from rocprofv3 --pmc counter CSVs.
+
+usage: python tools/pmc_traffic.py FETCH_counter_collection.csv WRITE_counter_collection.csv \
+           --kernel 'gemm_kernel<' --mode 1 --out profiles/traffic.json
+
+gfx950 corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE (KiB) reports exactly half of the bytes of wide
+coalesced streaming reads (16 B/lane loads and LDS-DMA alike) -> doubled; WRITE_SIZE (KiB) is exact for
+16-B-per-lane stores. Counters are collected in separate passes (one counter group per run)."""
+import argparse
+import csv
+import json
+import re
+from collections import defaultdict
+
+
+def load(path, counter):
+    per = defaultdict(float)
+    names = {}
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if r.get("Counter_Name") != counter:
+                continue
+            d = r.get("Dispatch_Id") or r.get("Correlation_Id")
+            per[d] += float(r["Counter_Value"])
+            names[d] = r.get("Kernel_Name", "")
+    return per, names
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch_csv")
+    ap.add_argument("write_csv")
+    ap.add_argument("--kernel", default="gemm_kernel<")
+    ap.add_argument("--mode", default="1", help="3rd template arg of gemm_kernel (1 = conv); '' = any")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    fetch, names = load(a.fetch_csv, "FETCH_SIZE")
+    write, wnames = load(a.write_csv, "WRITE_SIZE")
+    pat = re.compile(r"gemm_kernel<\d+, \d+, (\d+), \d+>")
+
+    def keep(n):
+        if a.kernel not in n:
+            return False
+        if a.mode == "":
+            return True
+        m = pat.search(n)
+        return bool(m) and m.group(1) == a.mode
+    f_sel = [v for d, v in fetch.items() if keep(names[d])]
+    w_sel = [v for d, v in write.items() if keep(wnames[d])]
+    if not f_sel or not w_sel:
+        raise SystemExit("no matching dispatches")
+    fetch_b = 2.0 * 1024 * sum(f_sel) / len(f_sel)   # gfx950: FETCH_SIZE counts half of wide reads
+    write_b = 1024 * sum(w_sel) / len(w_sel)
+    res = {"kernel": a.kernel, "mode": a.mode, "launches_fetch": len(f_sel), "launches_write": len(w_sel),
+           "fetch_bytes_per_launch": fetch_b, "write_bytes_per_launch": write_b,
+           "bytes_per_launch": fetch_b + write_b,
+           "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), WRITE_SIZE x1; KiB -> bytes"}
+    print(json.dumps(res, indent=1))
+    if a.out:
+        json.dump(res, open(a.out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
