@@ -22,8 +22,9 @@ namespace {
 
 constexpr int BK = 64;
 
-// tuning knobs (sdmoe_tune): 0 = LDS stages (0 = auto, 2 or 3)
+// tuning knobs (sdmoe_tune): 0 = LDS stages (0 = auto, 2 or 3); 1 = forced tile config (0 = auto)
 int g_stages = 0;
+int g_tile = 0;
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
@@ -82,22 +83,29 @@ SDMOE_DEV void epilogue8(const GemmParams& p, int m, int n, float (&v)[8]) {
 
 enum { MODE_GEMM = 0, MODE_CONV = 1, MODE_CONV_UP = 2 };
 
-template <int BM, int BN, int MODE, int NSTAGE>
-__global__ __launch_bounds__(256, (NSTAGE == 2 ? 2 : 1)) void gemm_kernel(GemmParams p) {
+template <int BM, int BN, int WMW, int WNW, int MODE, int NSTAGE>
+__global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 : 1)) void gemm_kernel(GemmParams p) {
   constexpr bool CONV = MODE != MODE_GEMM;
-  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int NW = WMW * WNW;                  // waves per workgroup
+  constexpr int WM = BM / WMW, WN = BN / WNW;    // per-wave output tile
   constexpr int FM = WM / 16, FN = WN / 16;
-  constexpr int A_PW = BM / 32, B_PW = BN / 32;  // LDS-DMA wave-instructions (8 rows each) per wave and stage
-  constexpr int PER_WAVE = A_PW + B_PW;
-  constexpr int STAGE = (BM + BN) * BK * 2;
+  static_assert(WM % 16 == 0 && WN % 16 == 0, "wave tile must be whole 16x16 fragments");
+  constexpr int A_INS = BM / 8, B_INS = BN / 8;  // 1-KiB LDS-DMA wave-instructions (8 rows) per stage
+  constexpr int A_PW = (A_INS + NW - 1) / NW, B_PW = (B_INS + NW - 1) / NW;
+  constexpr int PER_WAVE = A_PW + B_PW;          // every wave issues exactly this many (surplus -> dummy slot)
+  constexpr int STAGE_AB = (BM + BN) * BK * 2;
+  constexpr bool PADDED = (A_PW * NW != A_INS) || (B_PW * NW != B_INS);
+  constexpr int STAGE = STAGE_AB + (PADDED ? 1024 : 0);
   constexpr int WN_PAD = WN + 4;
-  constexpr int EPI = 4 * (WM / 2) * WN_PAD * 4;
+  constexpr int NPASS = (NW * (WM / 2) * WN_PAD * 4 <= NSTAGE * STAGE) ? 2 : ((NW * (WM / 4) * WN_PAD * 4 <= NSTAGE * STAGE) ? 4 : 8);
+  static_assert(FM % NPASS == 0, "epilogue passes must split the wave's fragment rows");
+  constexpr int EPI = NW * (WM / NPASS) * WN_PAD * 4;
   constexpr int SMEM = (NSTAGE * STAGE > EPI) ? NSTAGE * STAGE : EPI;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 1, wc = wave & 1;
+  const int wr = wave / WNW, wc = wave % WNW;
   const int ntn = (p.N + BN - 1) / BN, ntm = (p.M + BM - 1) / BM;
   const int bid = xcd_remap(blockIdx.x, ntn * ntm * p.ksplit);
   const int split = bid % p.ksplit, tile = bid / p.ksplit;
@@ -120,11 +128,11 @@ __global__ __launch_bounds__(256, (NSTAGE == 2 ? 2 : 1)) void gemm_kernel(GemmPa
   unsigned bvoff[B_PW];
 #pragma unroll
   for (int j = 0; j < A_PW; ++j) {
-    const int r = 8 * (wave * A_PW + j) + lrow;
+    const int r = 8 * (j * NW + wave) + lrow;
     const unsigned chb = (unsigned)((lch ^ swz(r)) * 16);
     const int m = m0 + r;
     avoff[j] = OOB; amask[j] = 0; aoh[j] = 0; aow[j] = 0; ab_[j] = 0;
-    if (m < p.M) {
+    if (j * NW + wave < A_INS && m < p.M) {
       if (MODE == MODE_GEMM) {
         avoff[j] = (unsigned)((long)m * p.lda * 2) + chb;
       } else {
@@ -149,10 +157,14 @@ __global__ __launch_bounds__(256, (NSTAGE == 2 ? 2 : 1)) void gemm_kernel(GemmPa
   }
 #pragma unroll
   for (int j = 0; j < B_PW; ++j) {
-    const int r = 8 * (wave * B_PW + j) + lrow;
+    const int r = 8 * (j * NW + wave) + lrow;
     const int n = n0 + r;
-    bvoff[j] = n < p.N ? (unsigned)((long)n * p.ldw * 2) + (unsigned)((lch ^ swz(r)) * 16) : OOB;
+    bvoff[j] = (j * NW + wave < B_INS && n < p.N) ? (unsigned)((long)n * p.ldw * 2) + (unsigned)((lch ^ swz(r)) * 16)
+                                                  : OOB;
   }
+  // LDS destination of wave-instruction j (surplus instructions of a padded tile land in a dummy 1-KiB slot)
+  auto a_dst = [&](int j) { return (j * NW + wave < A_INS) ? (j * NW + wave) * 1024 : STAGE_AB; };
+  auto b_dst = [&](int j) { return (j * NW + wave < B_INS) ? BM * BK * 2 + (j * NW + wave) * 1024 : STAGE_AB; };
 
   // conv K walk: (tap, 64-channel step) advanced incrementally in scalar registers
   const int csteps = CONV ? p.Cin / BK : 1;
@@ -160,11 +172,10 @@ __global__ __launch_bounds__(256, (NSTAGE == 2 ? 2 : 1)) void gemm_kernel(GemmPa
 
   auto issue_stage = [&](int ks, int buf) {
     char* sa = smem + buf * STAGE;
-    char* sbw = sa + BM * BK * 2;
     const unsigned kb = (unsigned)(ks * BK * 2);
     if (MODE == MODE_GEMM) {
 #pragma unroll
-      for (int j = 0; j < A_PW; ++j) bld16(rsA, sa + (wave * A_PW + j) * 1024, avoff[j], kb);
+      for (int j = 0; j < A_PW; ++j) bld16(rsA, sa + a_dst(j), avoff[j], kb);
     } else {
       const int tap = st_tap;
       const int kh = tap >= 6 ? 2 : (tap >= 3 ? 1 : 0);
@@ -176,7 +187,7 @@ __global__ __launch_bounds__(256, (NSTAGE == 2 ? 2 : 1)) void gemm_kernel(GemmPa
 #pragma unroll
         for (int j = 0; j < A_PW; ++j) {
           const unsigned vo = ((amask[j] >> tap) & 1u) ? avoff[j] + tapoff : OOB;
-          bld16(rsA, sa + (wave * A_PW + j) * 1024, vo, 0);
+          bld16(rsA, sa + a_dst(j), vo, 0);
         }
       } else {
 #pragma unroll
@@ -186,12 +197,12 @@ __global__ __launch_bounds__(256, (NSTAGE == 2 ? 2 : 1)) void gemm_kernel(GemmPa
           const unsigned vo =
               ok ? (unsigned)(((long)(ab_[j] * p.H + (uh >> 1)) * p.Wd + (uw >> 1)) * p.lda * 2) + avoff[j] + c0b
                  : OOB;
-          bld16(rsA, sa + (wave * A_PW + j) * 1024, vo, 0);
+          bld16(rsA, sa + a_dst(j), vo, 0);
         }
       }
     }
 #pragma unroll
-    for (int j = 0; j < B_PW; ++j) bld16(rsW, sbw + (wave * B_PW + j) * 1024, bvoff[j], kb);
+    for (int j = 0; j < B_PW; ++j) bld16(rsW, sa + b_dst(j), bvoff[j], kb);
   };
 
   float4v acc[FM][FN];
@@ -240,22 +251,22 @@ __global__ __launch_bounds__(256, (NSTAGE == 2 ? 2 : 1)) void gemm_kernel(GemmPa
   // 8-column chunks with 16-B (fp16) / 32-B (fp32 split-K slab) stores
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  float* st = reinterpret_cast<float*>(smem) + wave * (WM / 2) * WN_PAD;
+  float* st = reinterpret_cast<float*>(smem) + wave * (WM / NPASS) * WN_PAD;
   constexpr int CPR = WN / 8;
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < NPASS; ++h) {
 #pragma unroll
-    for (int i = 0; i < FM / 2; ++i)
+    for (int i = 0; i < FM / NPASS; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) st[(i * 16 + fg * 4 + r) * WN_PAD + j * 16 + fr] = acc[h * (FM / 2) + i][j][r];
+        for (int r = 0; r < 4; ++r) st[(i * 16 + fg * 4 + r) * WN_PAD + j * 16 + fr] = acc[h * (FM / NPASS) + i][j][r];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (int id = lane; id < (WM / 2) * CPR; id += 64) {
+    for (int id = lane; id < (WM / NPASS) * CPR; id += 64) {
       const int r = id / CPR, c8 = id - r * CPR;
-      const int m = m0 + wr * WM + h * (WM / 2) + r, n = n0 + wc * WN + c8 * 8;
+      const int m = m0 + wr * WM + h * (WM / NPASS) + r, n = n0 + wc * WN + c8 * 8;
       if (m >= p.M || n >= p.N) continue;
       const float* sp = st + r * WN_PAD + c8 * 8;
       float4v v0 = *reinterpret_cast<const float4v*>(sp), v1 = *reinterpret_cast<const float4v*>(sp + 4);
@@ -290,7 +301,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
   }
 }
 
-template <int BM, int BN, int MODE>
+template <int BM, int BN, int WMW, int WNW, int MODE>
 int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
   const int ntiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
   const int nk = p.K / BK;
@@ -305,11 +316,19 @@ int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
   p.ksplit = ksplit > 1 ? ksplit : 1;
   p.kchunk = (nk + p.ksplit - 1) / p.ksplit;
   p.part = p.ksplit > 1 ? ws : nullptr;
-  // 2-stage ring (2 workgroups/CU, latency hidden across workgroups) when the grid has >= ~300 workgroups;
-  // otherwise a 3-stage ring (1 workgroup/CU, two K-steps in flight) -- measured crossover on MI355X
-  int stages = g_stages ? g_stages : (ntiles * p.ksplit >= 300 ? 2 : 3);
-  if (stages == 2) gemm_kernel<BM, BN, MODE, 2><<<ntiles * p.ksplit, 256, 0, s>>>(p);
-  else gemm_kernel<BM, BN, MODE, 3><<<ntiles * p.ksplit, 256, 0, s>>>(p);
+  constexpr int NT = 64 * WMW * WNW;
+  // 4-wave tiles: 2-stage ring (2 workgroups/CU, latency hidden across workgroups) when the grid has >= ~300
+  // workgroups, else 3-stage (1 workgroup/CU, two K-steps in flight) -- measured crossover on MI355X.
+  // 8-wave tiles run one workgroup per CU either way: 3-stage where it fits in LDS (256x160), else 2-stage.
+  int stages = g_stages ? g_stages : ((WMW * WNW == 4 && ntiles * p.ksplit >= 300) ? 2 : 3);
+  constexpr bool FITS3 = 3 * ((BM + BN) * BK * 2 + 1024) <= 160 * 1024;
+  if constexpr (FITS3) {
+    if (stages == 2) gemm_kernel<BM, BN, WMW, WNW, MODE, 2><<<ntiles * p.ksplit, NT, 0, s>>>(p);
+    else gemm_kernel<BM, BN, WMW, WNW, MODE, 3><<<ntiles * p.ksplit, NT, 0, s>>>(p);
+  } else {
+    (void)stages;
+    gemm_kernel<BM, BN, WMW, WNW, MODE, 2><<<ntiles * p.ksplit, NT, 0, s>>>(p);
+  }
   SDMOE_CHECK_LAUNCH();
   if (p.ksplit > 1) {
     long nchunk = (long)p.M * (p.N / 8);
@@ -323,19 +342,32 @@ int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
 
 template <int MODE>
 int dispatch(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
-  if (MODE == MODE_CONV_UP) {  // only the 3 U-Net upsamplers: large M, N in {320, 640, 1280}
-    if (p.N % 160 == 0) return launch_tile<128, 160, MODE>(p, ws, ws_floats, s);
-    return launch_tile<128, 128, MODE>(p, ws, ws_floats, s);
-  }
+  const int tm256 = (p.M + 255) / 256;
+  // forced tile (sdmoe_tune knob 1): 1 = 128x160, 2 = 64x160, 3 = 256x320 (8 waves), 4 = 256x160 (8 waves)
+  if (g_tile == 1) return launch_tile<128, 160, 2, 2, MODE>(p, ws, ws_floats, s);
+  if (g_tile == 2) return launch_tile<64, 160, 2, 2, MODE>(p, ws, ws_floats, s);
+  if (g_tile == 3 && p.N % 320 == 0) return launch_tile<256, 320, 2, 4, MODE>(p, ws, ws_floats, s);
+  if (g_tile == 4 && p.N % 160 == 0) return launch_tile<256, 160, 4, 2, MODE>(p, ws, ws_floats, s);
+  // 8-wave 256x320 tile (wave tile 128x80: 2.5x the MFMA work per LDS byte of 64x80) whenever it alone fills
+  // the chip; 256x160 8-wave + split-K for long-K problems whose 128x160 grid is under ~1.2 waves of CUs.
+  // Measured on MI355X with tools/gemm_bench.py --tile.
+  const int nt320 = tm256 * (p.N / 320);
   const int nt160_128 = ((p.M + 127) / 128) * ((p.N + 159) / 160);
-  if (p.N <= 64) return launch_tile<128, 64, MODE>(p, ws, ws_floats, s);
+  if (p.N % 320 == 0 && nt320 >= 240) return launch_tile<256, 320, 2, 4, MODE>(p, ws, ws_floats, s);
+  if (p.N % 160 == 0 && p.K >= 2560 && nt160_128 < 300 && !(MODE == MODE_CONV && p.stride == 2))
+    return launch_tile<256, 160, 4, 2, MODE>(p, ws, ws_floats, s);
+  if (MODE == MODE_CONV_UP) {
+    if (p.N % 160 == 0) return launch_tile<128, 160, 2, 2, MODE>(p, ws, ws_floats, s);
+    return launch_tile<128, 128, 2, 2, MODE>(p, ws, ws_floats, s);
+  }
+  if (p.N <= 64) return launch_tile<128, 64, 2, 2, MODE>(p, ws, ws_floats, s);
   if (p.N % 160 == 0) {
-    if (nt160_128 >= 200 || p.M > 2048) return launch_tile<128, 160, MODE>(p, ws, ws_floats, s);
-    return launch_tile<64, 160, MODE>(p, ws, ws_floats, s);
+    if (nt160_128 >= 200 || p.M > 2048) return launch_tile<128, 160, 2, 2, MODE>(p, ws, ws_floats, s);
+    return launch_tile<64, 160, 2, 2, MODE>(p, ws, ws_floats, s);
   }
   const int nt128 = ((p.M + 127) / 128) * ((p.N + 127) / 128);
-  if (nt128 >= 200 || p.M > 2048) return launch_tile<128, 128, MODE>(p, ws, ws_floats, s);
-  return launch_tile<64, 128, MODE>(p, ws, ws_floats, s);
+  if (nt128 >= 200 || p.M > 2048) return launch_tile<128, 128, 2, 2, MODE>(p, ws, ws_floats, s);
+  return launch_tile<64, 128, 2, 2, MODE>(p, ws, ws_floats, s);
 }
 
 // ---- elementwise helpers for the GEMM operands ------------------------------------------------------
@@ -455,5 +487,6 @@ extern "C" int sdmoe_mask_weight(const void* W, const void* bits, long N, long K
 
 extern "C" int sdmoe_tune(int knob, int value) {
   if (knob == 0 && (value == 0 || value == 2 || value == 3)) { g_stages = value; return SDMOE_OK; }
+  if (knob == 1 && value >= 0 && value <= 4) { g_tile = value; return SDMOE_OK; }
   return SDMOE_EARG;
 }

@@ -118,7 +118,8 @@ int sdmoe_prepare_input(const float* lat, void* out, int B, int HW, long ldo, in
 int sdmoe_cfg_ddim_step(const void* eps, long lde, float* lat, int B, int HW, int do_cfg, float guidance,
                         float alpha_t, float alpha_prev, void* next_in, long ldn, void* stream);
 
-/* Tuning knobs for A/B experiments: knob 0 = GEMM LDS pipeline stages (2 or 3). */
+/* Tuning knobs for A/B experiments: knob 0 = GEMM LDS pipeline stages (0 auto, 2 or 3); knob 1 = forced GEMM tile
+   (0 auto, 1 = 128x160, 2 = 64x160, 3 = 256x320 8-wave, 4 = 256x160 8-wave). */
 int sdmoe_tune(int knob, int value);
 
 /* out = a + b (fp16, n % 8 == 0). */

@@ -131,6 +131,26 @@ def test_conv3x3_strided_concat_input():
     close(ops.conv3x3(buf[:, C1:], nimg, H, H, w2, b), conv_ref(buf[:, C1:].contiguous(), nimg, H, H, w2, b))
 
 
+@pytest.mark.parametrize("tile", [1, 2, 3, 4])
+def test_forced_tiles(tile):
+    """Every tile configuration of the GEMM kernel (sdmoe_tune knob 1), in all three modes, with ragged M."""
+    from sdmoe import _lib
+    lib = _lib.load()
+    _lib.check(lib.sdmoe_tune(1, tile), "tune")
+    try:
+        x = rnd(1000, 640, seed=40)
+        w = rnd(1280, 640, scale=640 ** -0.5, seed=41)
+        b = rnd(1280, scale=0.1, seed=42)
+        close(ops.linear(x, w, b, act=ops.ACT_GELU), F.gelu(x.float() @ w.float().t() + b.float()))
+        for Cin, Cout, H, st, up in [(320, 640, 12, 1, False), (640, 320, 8, 1, True), (320, 320, 12, 2, False)]:
+            xi = rnd(2 * H * H, Cin, seed=43)
+            wi = rnd(Cout, 3, 3, Cin, scale=(9 * Cin) ** -0.5, seed=44)
+            bi = rnd(Cout, scale=0.1, seed=45)
+            close(ops.conv3x3(xi, 2, H, H, wi, bi, stride=st, upsample=up), conv_ref(xi, 2, H, H, wi, bi, st, up))
+    finally:
+        _lib.check(lib.sdmoe_tune(1, 0), "tune")
+
+
 @pytest.mark.parametrize("C,HW,eps", [(320, 4096, 1e-5), (960, 256, 1e-6), (2560, 64, 1e-5), (1920, 1024, 1e-5)])
 def test_groupnorm_stats(C, HW, eps):
     nimg = 2

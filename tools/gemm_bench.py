@@ -30,10 +30,13 @@ def main():
     ap.add_argument("--nimg", type=int, default=16)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--stages", type=int, default=0)
+    ap.add_argument("--tile", type=int, default=0, help="forced GEMM tile (sdmoe_tune knob 1), 0 = auto")
+    ap.add_argument("--only", default="", help="run only rows whose label contains this")
     a = ap.parse_args()
     from sdmoe import _lib
     _lib.check(_lib.load().sdmoe_tune(0, a.stages), "tune")
-    print("stages", a.stages)
+    _lib.check(_lib.load().sdmoe_tune(1, a.tile), "tune")
+    print("stages", a.stages, "tile", a.tile)
     n = a.nimg
     dev = "cuda"
     rows = []
@@ -68,6 +71,8 @@ def main():
         ms = timeit(f, a.iters)
         rows.append((f"attn N={N_} d={d} Nk={Nk}", ms, 4.0 * n * 8 * N_ * Nk * d / ms / 1e9))
     for name, ms, tf in rows:
+        if a.only and a.only not in name:
+            continue
         print(f"{name:42s} {ms*1e3:9.1f} us {tf:8.1f} TF/s")
 
 
