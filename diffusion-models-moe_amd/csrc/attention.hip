@@ -12,7 +12,10 @@
 //   * the S^T accumulator, converted to fp16, is directly the B operand of O^T = V^T P^T with a key
 //     permutation inside each 32-key slot; V^T comes out of LDS with ds_read_b64_tr_b16 (gfx950 transpose
 //     read), with the same permutation, so no LDS round trip for P;
-//   * K/V tiles of 64 keys are register-prefetched (issue before the tile's MFMAs, LDS write after).
+//   * K/V tiles of 64 keys arrive by LDS-DMA (buffer_load ... lds, out-of-range keys and padding slots read
+//     as zeros) into a double-buffered ring: tile kt+1 is issued before tile kt's MFMAs, one barrier per tile.
+#include <type_traits>
+
 #include "common.h"
 #include "../../include/sdmoe.h"
 
@@ -33,24 +36,56 @@ SDMOE_DEV half4 ds_read_tr(const half_t* p) {
   return __builtin_bit_cast(half4, v);
 }
 
+// This file is compiled with -fno-honor-nans (csrc/Makefile): fmaxf chains on MFMA results then lower to
+// v_max3_f32 without a canonicalising v_max in front of each operand. (Inline-asm v_max3 is not an option:
+// the hazard recognizer does not pad an asm VALU read of a just-written MFMA result.)
+SDMOE_DEV float max3(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
+SDMOE_DEV float max2(float a, float b) { return fmaxf(a, b); }
+// max over the 4 lanes {l, l^16, l^32, l^48} with the gfx950 cross-row swaps (no LDS round trip)
+SDMOE_DEV float max_xrows(float v) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = max2(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  auto t = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return max2(__uint_as_float(t[0]), __uint_as_float(t[1]));
+}
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+SDMOE_DEV void bld16(__amdgpu_buffer_rsrc_t rs, const half_t* lds_dst, unsigned voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)lds_dst, 16, voff, 0, 0, 0);
+}
+
 template <int D>
 __global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn_fwd_kernel(AttnParams p) {
   constexpr int DK = ((D + 31) / 32) * 32;   // contraction dim padded for 16x16x32
   constexpr int DV = ((D + 15) / 16) * 16;   // output dim padded to 16-row fragments
   constexpr int KB = 64;                      // keys per tile
-  constexpr int KS = DK + 8;                  // K row stride (halves): +16 B pad -> conflict-free b128
-  constexpr int VS = DV + 4;                  // V row stride (halves): 8-B aligned rows for tr reads
+  // K and V row stride (halves) in LDS: the smallest odd multiple of 16 >= D (48, 80, 176 for D = 40, 80, 160)
+  // makes both the ds_read_b128 K-fragment reads and the ds_read_b64_tr_b16 V^T reads bank-conflict-free. A K
+  // row may be shorter than DK: the fragment read of columns D..DK-1 then runs into the next row (or the
+  // zeroed tail), harmless because the matching Q columns are zero.
+  constexpr int RS = ((D + 15) / 16) % 2 ? ((D + 15) / 16) * 16 : ((D + 15) / 16) * 16 + 16;
   constexpr int NDC = DK / 32, NDF = DV / 16;
-  constexpr int CH = D / 8;                   // 16-B chunks per row
-  constexpr int TOT = KB * CH;
-  constexpr int PER = (TOT + 255) / 256;
-  constexpr bool SUM_BY_MFMA = DV > D;     // V column D = 1.0 -> O^T row D accumulates sum_k P[k][q]
+  constexpr int CH = D / 8;                   // real 16-B chunks per row
+  constexpr int SL = RS / 8;                  // 16-B LDS slots per row (SL - CH padding slots, loaded as zeros)
+  constexpr int TILE = KB * RS;               // halves per K (or V) tile image
+  constexpr int NPIECE = TILE * 2 / 1024;     // 1-KiB LDS-DMA wave-instructions per K (or V) tile
+  constexpr int NPW = 2 * NPIECE / 4;         // per wave, K and V together
+  static_assert((2 * NPIECE) % 4 == 0, "K+V pieces must split evenly over the 4 waves");
+  constexpr int KBUF = TILE + 64;             // + zeroed tail for the over-read of the last K row
+  constexpr bool SUM_BY_MFMA = DV > D;        // O^T row D accumulates sum_k P[k][q] (V column D := 1.0)
+  static_assert(!SUM_BY_MFMA || D % 16 == 8, "ones column sits at the start of a 4-column tr-read group");
   constexpr float RESCALE_THR = 8.0f;
+  constexpr unsigned OOB = 0x80000000u;
 
-  __shared__ __attribute__((aligned(16))) half_t Ks[KB * KS];
-  __shared__ __attribute__((aligned(16))) half_t Vs[KB * VS];
+  // separate arrays per ring slot: with the slot a compile-time constant the compiler can tell the DMA into
+  // one slot from the ds_reads of the other and does not drain vmcnt in front of every LDS read
+  // slot layout: [K tile | zero tail | V tile | 1 0 0 0 0 0 0 0]
+  constexpr int SLOT = KBUF + TILE + 8;
+  __shared__ __attribute__((aligned(1024))) half_t S0[SLOT];
+  __shared__ __attribute__((aligned(1024))) half_t S1[SLOT];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, w = lane & 15;
   const int b = blockIdx.z, h = blockIdx.y;
   const int q0 = blockIdx.x * 128 + wave * 32;
@@ -58,18 +93,43 @@ __global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn_fwd_kernel(AttnP
   const half_t* Qb = p.Q + (long)b * p.Nq * p.ldq + h * D;
   const half_t* Kb = p.K + (long)b * p.Nk * p.ldk + h * D;
   const half_t* Vb = p.V + (long)b * p.Nk * p.ldv + h * D;
+  // buffer resources end at the last key's row: keys >= Nk (ragged last tile) read as zeros
+  const __amdgpu_buffer_rsrc_t rsK =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Kb, (short)0, (int)(((long)p.Nk - 1) * p.ldk * 2 + D * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsV =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Vb, (short)0, (int)(((long)p.Nk - 1) * p.ldv * 2 + D * 2), 0x00020000);
 
-  // zero the padding columns once (tiles never write them)
-  for (int i = tid; i < KB * (KS - D); i += 256) {
-    int r = i / (KS - D), c = D + i % (KS - D);
-    Ks[r * KS + c] = (half_t)0.f;
+  // per-wave LDS-DMA pieces: global piece gp = wave + 4j (K pieces first, then V); lane = one 16-B slot
+  unsigned voff[NPW], vstep[NPW];
+  int ldsoff[NPW];
+#pragma unroll
+  for (int j = 0; j < NPW; ++j) {
+    const int gp = wave + 4 * j;
+    const bool isk = gp < NPIECE;
+    const int pc = isk ? gp : gp - NPIECE;
+    const int slot = pc * 64 + lane, r = slot / SL, c = slot - (slot / SL) * SL;
+    const long ld = isk ? p.ldk : p.ldv;
+    voff[j] = c < CH ? (unsigned)(r * ld * 2 + c * 16) : OOB;
+    vstep[j] = (unsigned)(KB * ld * 2);
+    ldsoff[j] = (isk ? 0 : KBUF) + pc * 512;
   }
-  for (int i = tid; i < KB * (VS - D); i += 256) {
-    int r = i / (VS - D), c = D + i % (VS - D);
-    Vs[r * VS + c] = (half_t)((SUM_BY_MFMA && c == D) ? 1.f : 0.f);
-  }
+  auto issue_tile = [&](half_t* Sd) {  // DMA the tile at the current voff into ring slot Sd, advance voff
+#pragma unroll
+    for (int j = 0; j < NPW; ++j) {
+      bld16(wave + 4 * j < NPIECE ? rsK : rsV, Sd + ldsoff[j], voff[j]);
+      voff[j] += vstep[j];
+    }
+  };
 
-  // Q fragments (B operand of S^T = K Q^T): lane holds Q[q = w][d = 32c + 8g + j]
+  // zeroed over-read tails, the constant [1 0 0 0 | 0 0 0 0] block the V^T reads of the ones column use
+  for (int i = tid; i < KBUF - TILE; i += 256) S0[TILE + i] = S1[TILE + i] = 0;
+  if (tid < 8) S0[KBUF + TILE + tid] = S1[KBUF + TILE + tid] = (half_t)(tid == 0 ? 1.f : 0.f);
+
+  const int nkt = (p.Nk + KB - 1) / KB;
+  issue_tile(S0);
+
+  // Q fragments (B operand of S^T = K Q^T), pre-multiplied by scale*log2(e) so that the score accumulator is
+  // already the exp2 argument: lane holds Q[q = w][d = 32c + 8g + j]
   half8 qf[2][NDC];
 #pragma unroll
   for (int f = 0; f < 2; ++f)
@@ -78,6 +138,8 @@ __global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn_fwd_kernel(AttnP
       const int q = q0 + f * 16 + w, d = 32 * c + 8 * g;
       half8 v = {0, 0, 0, 0, 0, 0, 0, 0};
       if (q < p.Nq && d < D) v = *reinterpret_cast<const half8*>(Qb + (long)q * p.ldq + d);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (half_t)((float)v[j] * p.scale_log2);
       qf[f][c] = v;
     }
 
@@ -86,104 +148,87 @@ __global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn_fwd_kernel(AttnP
   for (int f = 0; f < 2; ++f)
 #pragma unroll
     for (int d = 0; d < NDF; ++d) oacc[f][d] = (float4v){0.f, 0.f, 0.f, 0.f};
-  float mrun[2] = {-1e30f, -1e30f}, lrun[2] = {0.f, 0.f};
+  float mrun[2] = {0.f, 0.f}, lrun[2] = {0.f, 0.f};
 
-  uint4v rk[PER], rv[PER];
-  auto load_tile = [&](int kt) {
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int id = tid + 256 * i;
-      uint4v a = {0u, 0u, 0u, 0u}, c = {0u, 0u, 0u, 0u};
-      if (id < TOT) {
-        const int r = id / CH, ch = id - r * CH;
-        const int key = kt * KB + r;
-        if (key < p.Nk) {
-          a = *reinterpret_cast<const uint4v*>(Kb + (long)key * p.ldk + ch * 8);
-          c = *reinterpret_cast<const uint4v*>(Vb + (long)key * p.ldv + ch * 8);
-        }
-      }
-      rk[i] = a; rv[i] = c;
-    }
-  };
-  auto store_tile = [&]() {
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int id = tid + 256 * i;
-      if (id < TOT) {
-        const int r = id / CH, ch = id - r * CH;
-        *reinterpret_cast<uint4v*>(Ks + r * KS + ch * 8) = rk[i];
-        // V rows are only 8-B aligned (VS*2 bytes): store as two 8-B halves
-        uint2* vd = reinterpret_cast<uint2*>(Vs + r * VS + ch * 8);
-        vd[0] = (uint2){rv[i][0], rv[i][1]};
-        vd[1] = (uint2){rv[i][2], rv[i][3]};
-      }
-    }
+  // V^T fragment addresses (tr reads, key slots permuted to match P); lanes of the ones-column group read the
+  // constant block instead
+  const int tq = w >> 2, tp = w & 3;
+  auto vaddr = [&](const half_t* Vt, int c2, int hi, int df) -> const half_t* {
+    const int normal = (32 * c2 + 16 * hi + 4 * g + tq) * RS + 16 * df + 4 * tp;
+    if (SUM_BY_MFMA && df == D / 16) return Vt + (4 * tp >= D % 16 ? TILE + (4 * tp == D % 16 ? 0 : 4) : normal);
+    return Vt + normal;
   };
 
-  const int nkt = (p.Nk + KB - 1) / KB;
-  load_tile(0);
-  __syncthreads();
-  store_tile();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  for (int kt = 0; kt < nkt; ++kt) {
-    if (kt + 1 < nkt) load_tile(kt + 1);
+  auto tile = [&](int kt, auto ragged_tag, auto buf_tag) {
+    constexpr bool RAGGED = decltype(ragged_tag)::value;
+    constexpr int BUF = decltype(buf_tag)::value;
+    const half_t* Kt = BUF ? S1 : S0;
+    const half_t* Vt = Kt + KBUF;
+    // the other slot was last read in tile kt-1, which every wave finished before the previous barrier
+    if (kt + 1 < nkt) issue_tile(BUF ? S0 : S1);
 
-    // ---- S^T = K Q^T for the 4 key fragments of this tile
+    // ---- S'^T = K Q~^T - m: the accumulator starts at -m (running max, log2 units), so after the MFMAs it
+    //      holds exp2's argument directly (tile 0 starts at 0 and sets m from its own max)
     float4v s[2][4];
 #pragma unroll
-    for (int f = 0; f < 2; ++f)
+    for (int f = 0; f < 2; ++f) {
+      const float nm = -mrun[f];
 #pragma unroll
-      for (int kf = 0; kf < 4; ++kf) s[f][kf] = (float4v){0.f, 0.f, 0.f, 0.f};
+      for (int kf = 0; kf < 4; ++kf) s[f][kf] = (float4v){nm, nm, nm, nm};
+    }
 #pragma unroll
     for (int kf = 0; kf < 4; ++kf)
 #pragma unroll
       for (int c = 0; c < NDC; ++c) {
-        half8 a = *reinterpret_cast<const half8*>(Ks + (kf * 16 + w) * KS + 32 * c + 8 * g);
+        half8 a = *reinterpret_cast<const half8*>(Kt + (kf * 16 + w) * RS + 32 * c + 8 * g);
 #pragma unroll
         for (int f = 0; f < 2; ++f) s[f][kf] = mfma16x16x32(a, qf[f][c], s[f][kf]);
       }
 
-    // ---- online softmax (query on the lane), VALU-lean:
-    //  * raw-score max (scale > 0 commutes with max), scale folded into the exp2 argument: p = 2^(s*c - m);
-    //  * key masking only on the ragged last tile (uniform branch);
-    //  * deferred rescale: the running max moves only when some query's tile max exceeds it by > RESCALE_THR
-    //    (log2 units), so most tiles skip the O/l rescale; p <= 2^RESCALE_THR stays well inside fp16;
-    //  * for D with a pad column (D = 40) the row sum comes out of the PV MFMA (V pad column = 1.0).
-    const int kbase = kt * KB;
-    const bool ragged = kbase + KB > p.Nk;
+    // ---- online softmax (query on the lane), VALU-lean: per score one exp2, a third of a max3 and half a
+    //      cvt_pk; deferred rescale (m moves only when a tile max exceeds it by > RESCALE_THR, log2 units, so
+    //      p <= 2^8 stays well inside fp16); masking only in the peeled ragged last tile
     half8 pb[2][2];
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
-      if (ragged) {
+      if constexpr (RAGGED) {
 #pragma unroll
         for (int kf = 0; kf < 4; ++kf)
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            if (kbase + kf * 16 + 4 * g + i >= p.Nk) s[f][kf][i] = -INFINITY;
+            if (kt * KB + kf * 16 + 4 * g + i >= p.Nk) s[f][kf][i] = -INFINITY;
       }
-      float mx = fmaxf(fmaxf(s[f][0][0], s[f][0][1]), fmaxf(s[f][0][2], s[f][0][3]));
+      float m0 = max3(s[f][0][0], s[f][0][1], s[f][0][2]);
+      float m1 = max3(s[f][0][3], s[f][1][0], s[f][1][1]);
+      float m2 = max3(s[f][1][2], s[f][1][3], s[f][2][0]);
+      float m3 = max3(s[f][2][1], s[f][2][2], s[f][2][3]);
+      float m4 = max3(s[f][3][0], s[f][3][1], s[f][3][2]);
+      m0 = max3(m0, m1, s[f][3][3]);
+      m2 = max3(m2, m3, m4);
+      const float mx = max_xrows(max2(m0, m2));
+      if (kt == 0) {  // first tile: m = its max (O and l are still zero)
+        mrun[f] = mx;
 #pragma unroll
-      for (int kf = 1; kf < 4; ++kf)
-        mx = fmaxf(mx, fmaxf(fmaxf(s[f][kf][0], s[f][kf][1]), fmaxf(s[f][kf][2], s[f][kf][3])));
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mxs = mx * p.scale_log2;
-      if (!__all(mxs - mrun[f] <= RESCALE_THR)) {  // wave-uniform decision
-        const float mnew = fmaxf(mrun[f], mxs);
-        const float alpha = __builtin_amdgcn_exp2f(mrun[f] - mnew);
-        mrun[f] = mnew;
+        for (int kf = 0; kf < 4; ++kf) s[f][kf] -= mx;
+      } else if (!__all(mx <= RESCALE_THR)) {  // wave-uniform decision
+        const float delta = fmaxf(mx, 0.f);
+        mrun[f] += delta;
+        const float alpha = __builtin_amdgcn_exp2f(-delta);
         if (!SUM_BY_MFMA) lrun[f] *= alpha;
 #pragma unroll
         for (int d = 0; d < NDF; ++d) oacc[f][d] *= alpha;
+#pragma unroll
+        for (int kf = 0; kf < 4; ++kf) s[f][kf] -= delta;
       }
-      const float nm = -mrun[f];
       float ls = 0.f;
 #pragma unroll
       for (int kf = 0; kf < 4; ++kf)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(s[f][kf][i], p.scale_log2, nm));
+          const float e = __builtin_amdgcn_exp2f(s[f][kf][i]);
           s[f][kf][i] = e;
           if (!SUM_BY_MFMA) ls += e;
         }
@@ -200,22 +245,36 @@ __global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn_fwd_kernel(AttnP
       }
     }
 
-    // ---- O^T += V^T P^T (V^T via transpose reads, key slots permuted to match P)
-    const int tq = w >> 2, tp = w & 3;
+    // ---- O^T += V^T P^T
 #pragma unroll
     for (int c2 = 0; c2 < 2; ++c2)
 #pragma unroll
       for (int df = 0; df < NDF; ++df) {
-        half4 lo = ds_read_tr(Vs + (32 * c2 + 4 * g + tq) * VS + 16 * df + 4 * tp);
-        half4 hi = ds_read_tr(Vs + (32 * c2 + 16 + 4 * g + tq) * VS + 16 * df + 4 * tp);
+        half4 lo = ds_read_tr(vaddr(Vt, c2, 0, df));
+        half4 hi = ds_read_tr(vaddr(Vt, c2, 1, df));
         half8 a = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 #pragma unroll
         for (int f = 0; f < 2; ++f) oacc[f][df] = mfma16x16x32(a, pb[f][c2], oacc[f][df]);
       }
 
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of tile kt+1 have landed
     __syncthreads();
-    if (kt + 1 < nkt) store_tile();
-    __syncthreads();
+  };
+
+  using F_ = std::integral_constant<bool, false>;
+  using T_ = std::integral_constant<bool, true>;
+  using B0 = std::integral_constant<int, 0>;
+  using B1 = std::integral_constant<int, 1>;
+  const int nfull = p.Nk / KB;
+  int kt = 0;
+  for (; kt + 1 < nfull; kt += 2) {  // unrolled by the two ring slots
+    tile(kt, F_(), B0());
+    tile(kt + 1, F_(), B1());
+  }
+  if (kt < nfull) { tile(kt, F_(), B0()); ++kt; }
+  if (kt < nkt) {
+    if (kt & 1) tile(kt, T_(), B1());
+    else tile(kt, T_(), B0());
   }
 
   // ---- normalise and store O[q][d] (lane: query w, rows d = 16df + 4g + i)
