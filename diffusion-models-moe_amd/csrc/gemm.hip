@@ -43,6 +43,12 @@ struct GemmParams {
   int H, Wd, Cin, OH, OW, stride, upsample;
   int ksplit, kchunk;
   int a_bytes, w_bytes;  // SRD num_records
+  // routed-GEGLU epilogue (sdmoe_linear_geglu): W rows interleaved [value 8 | gate 8] per 8-neuron chunk, C is
+  // the [M, N/2] product value * act(gate); score [M, ld_score] gets per-expert sums of act(gate) over
+  // contiguous esize-neuron experts (neurons pre-permuted so every expert is contiguous)
+  int geglu;
+  half_t* score; long ld_score;
+  int esize;
 };
 
 SDMOE_DEV int swz(int row) { return (row >> 1) & 7; }
@@ -82,6 +88,43 @@ SDMOE_DEV void epilogue8(const GemmParams& p, int m, int n, float (&v)[8]) {
 }
 
 enum { MODE_GEMM = 0, MODE_CONV = 1, MODE_CONV_UP = 2 };
+
+// Routed-GEGLU epilogue over one staged pass (rows x WN fp32 in LDS, row stride WN_PAD) of a wave's tile
+// whose columns n0..n0+WN-1 are [value 8 | gate 8] chunk pairs. Rounds exactly like the unfused path
+// (fp16 linear output, fp16 act, fp16 product; expert score = fp32 sum in neuron order, rounded to fp16).
+template <int WN, int WN_PAD>
+SDMOE_DEV void geglu_pass(const GemmParams& p, const float* st, int mrow0, int rows, int n0, int lane) {
+  constexpr int PPR = WN / 16;  // chunk pairs per row
+  for (int id = lane; id < rows * PPR; id += 64) {
+    const int r = id / PPR, j = id - r * PPR;
+    const int m = mrow0 + r, n = n0 + 16 * j;
+    if (m >= p.M) continue;
+    const float* sp = st + r * WN_PAD + 16 * j;
+    const half8 bh = *reinterpret_cast<const half8*>(p.bias + n);
+    const half8 bg = *reinterpret_cast<const half8*>(p.bias + n + 8);
+    half8 o;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const half_t yh = (half_t)(sp[t] + (float)bh[t]);
+      const half_t ga = (half_t)apply_act((float)(half_t)(sp[8 + t] + (float)bg[t]), p.act);
+      o[t] = (half_t)((float)yh * (float)ga);
+    }
+    *reinterpret_cast<half8*>(p.C + (long)m * p.ldc + n / 2) = o;
+  }
+  if (!p.score) return;
+  const int S = p.esize, NE = (WN / 2) / S;
+  for (int id = lane; id < rows * NE; id += 64) {
+    const int r = id / NE, e = id - r * NE;
+    const int m = mrow0 + r;
+    if (m >= p.M) continue;
+    float acc = 0.f;
+    for (int t = e * S; t < (e + 1) * S; ++t) {
+      const int col = 16 * (t >> 3) + 8 + (t & 7);
+      acc += (float)(half_t)apply_act((float)(half_t)(st[r * WN_PAD + col] + (float)p.bias[n0 + col]), p.act);
+    }
+    p.score[(long)m * p.ld_score + n0 / 2 / S + e] = (half_t)acc;
+  }
+}
 
 template <int BM, int BN, int WMW, int WNW, int MODE, int NSTAGE>
 __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 : 1)) void gemm_kernel(GemmParams p) {
@@ -264,6 +307,9 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (p.geglu) {
+      geglu_pass<WN, WN_PAD>(p, st, m0 + wr * WM + h * (WM / NPASS), WM / NPASS, n0 + wc * WN, lane);
+    } else
     for (int id = lane; id < (WM / NPASS) * CPR; id += 64) {
       const int r = id / CPR, c8 = id - r * CPR;
       const int m = m0 + wr * WM + h * (WM / NPASS) + r, n = n0 + wc * WN + c8 * 8;
@@ -338,6 +384,15 @@ int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
     SDMOE_CHECK_LAUNCH();
   }
   return SDMOE_OK;
+}
+
+// routed-GEGLU linear: BN in {160, 320} tiles only (wave tile width 80 = 40 neurons = whole experts), no split-K
+int dispatch_geglu(const GemmParams& p, hipStream_t s) {
+  const int nt320 = ((p.M + 255) / 256) * (p.N / 320);
+  const int nt160_128 = ((p.M + 127) / 128) * (p.N / 160);
+  if (p.N % 320 == 0 && nt320 >= 240) return launch_tile<256, 320, 2, 4, MODE_GEMM>(p, nullptr, 0, s);
+  if (nt160_128 >= 200 || p.M > 2048) return launch_tile<128, 160, 2, 2, MODE_GEMM>(p, nullptr, 0, s);
+  return launch_tile<64, 160, 2, 2, MODE_GEMM>(p, nullptr, 0, s);
 }
 
 template <int MODE>
@@ -438,6 +493,25 @@ extern "C" int sdmoe_linear(const void* A, long lda, const void* W, long ldw, co
   if (ab >= (long)OOB || wb >= (long)OOB) return SDMOE_ESHAPE;
   p.a_bytes = (int)ab; p.w_bytes = (int)wb;
   return dispatch<MODE_GEMM>(p, workspace, workspace_floats, (hipStream_t)stream);
+}
+
+extern "C" int sdmoe_linear_geglu(const void* A, long lda, const void* W, long ldw, const void* bias, void* P,
+                                  long ldp, int M, int F, int K, int act, void* score, long ld_score, int esize,
+                                  void* stream) {
+  if (!A || !W || !bias || !P || M < 0 || F <= 0 || K <= 0) return SDMOE_EARG;
+  if (M == 0) return SDMOE_OK;
+  if (K % 64 || F % 80 || lda % 8 || ldw % 8 || ldp % 8) return SDMOE_ESHAPE;
+  if (score && (esize <= 0 || 40 % esize || ld_score < F / esize)) return SDMOE_ESHAPE;
+  if (!(act == ACT_GELU || act == ACT_RELU || act == ACT_NONE || act == ACT_SILU)) return SDMOE_EUNSUP;
+  GemmParams p{};
+  p.A = (const half_t*)A; p.lda = lda; p.W = (const half_t*)W; p.ldw = ldw;
+  p.bias = (const half_t*)bias; p.C = (half_t*)P; p.ldc = ldp;
+  p.M = M; p.N = 2 * F; p.K = K; p.act = act; p.rows_per_batch = 1;
+  p.geglu = 1; p.score = (half_t*)score; p.ld_score = ld_score; p.esize = esize;
+  const long ab = ((long)(M - 1) * lda + K) * 2, wb = ((long)(2 * F - 1) * ldw + K) * 2;
+  if (ab >= (long)OOB || wb >= (long)OOB) return SDMOE_ESHAPE;
+  p.a_bytes = (int)ab; p.w_bytes = (int)wb;
+  return dispatch_geglu(p, (hipStream_t)stream);
 }
 
 extern "C" int sdmoe_conv3x3(const void* X, long ldx, int nimg, int H, int W, int Cin,

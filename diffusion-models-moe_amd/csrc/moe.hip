@@ -140,7 +140,103 @@ __global__ __launch_bounds__(256) void geglu_route_kernel(RouteParams p) {
   }
 }
 
+// Top-k expert mask over a routed-GEGLU product computed by sdmoe_linear_geglu (experts contiguous, esize
+// neurons each): per token, scores (fp16, removed experts -> 0) -> the same radix top-k as above -> zero the
+// neurons of every expert that is not selected (or is removed). One wave per token; only zeros are written.
+template <int SLOTS>
+__global__ __launch_bounds__(256) void moe_topk_mask_kernel(half_t* __restrict__ P, long ldp, int M, int F, int E,
+                                                            int S, int k, const half_t* __restrict__ score,
+                                                            long lds, const uint32_t* __restrict__ removed,
+                                                            uint32_t* __restrict__ sel_out) {
+  __shared__ uint32_t selw_all[4][8];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t* selw = selw_all[wave];
+  const int m = blockIdx.x * 4 + wave;
+  if (m >= M) return;  // wave-uniform; no block-level barrier below
+  const int nw = (E + 31) >> 5;
+  uint32_t key[SLOTS];
+  bool valid[SLOTS];
+#pragma unroll
+  for (int i = 0; i < SLOTS; ++i) {
+    const int e = lane + 64 * i;
+    valid[i] = e < E;
+    half_t sc = valid[i] ? score[(long)m * lds + e] : (half_t)0.f;
+    if (valid[i] && removed && ((removed[e >> 5] >> (e & 31)) & 1u)) sc = (half_t)0.f;
+    key[i] = valid[i] ? order_key(sc) : 0u;
+  }
+  uint32_t T = 0;
+  for (int bit = 15; bit >= 0; --bit) {
+    const uint32_t cand = T | (1u << bit);
+    int cnt = 0;
+#pragma unroll
+    for (int i = 0; i < SLOTS; ++i) cnt += __popcll(__ballot(valid[i] && key[i] >= cand));
+    if (cnt >= k) T = cand;
+  }
+  int gt = 0;
+#pragma unroll
+  for (int i = 0; i < SLOTS; ++i) gt += __popcll(__ballot(valid[i] && key[i] > T));
+  const int need = k - gt;
+  const unsigned long long below = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
+  int rank_base = 0;
+#pragma unroll
+  for (int i = 0; i < SLOTS; ++i) {
+    const bool tie = valid[i] && key[i] == T;
+    const unsigned long long tm = __ballot(tie);
+    const bool sel = k > 0 && valid[i] && (key[i] > T || (tie && rank_base + __popcll(tm & below) < need));
+    rank_base += __popcll(tm);
+    const unsigned long long sm = __ballot(sel);
+    if (lane == 0) {
+      if (2 * i < 8) selw[2 * i] = (uint32_t)sm;
+      if (2 * i + 1 < 8) selw[2 * i + 1] = (uint32_t)(sm >> 32);
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (sel_out && lane < nw) sel_out[(long)m * nw + lane] = selw[lane];
+  uint32_t keepw[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) keepw[i] = (i < nw) ? selw[i] & (removed ? ~removed[i] : ~0u) : 0u;
+  half_t* row = P + (long)m * ldp;
+  for (int c = lane; c < (F >> 3); c += 64) {
+    unsigned kb = 0;  // keep bit per neuron of this 8-neuron chunk
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int e = (8 * c + j) / S;
+      kb |= ((keepw[e >> 5] >> (e & 31)) & 1u) << j;
+    }
+    if (kb == 0xffu) continue;
+    half8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (kb) {
+      v = *reinterpret_cast<const half8*>(row + 8 * c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (!((kb >> j) & 1u)) v[j] = (half_t)0.f;
+    }
+    *reinterpret_cast<half8*>(row + 8 * c) = v;
+  }
+}
+
 }  // namespace
+
+extern "C" int sdmoe_moe_topk_mask(void* P, long ldp, int M, int F, int E, int esize, int k, const void* score,
+                                   long ld_score, const unsigned* removed_bits, unsigned* sel_out, void* stream) {
+  if (!P || !score || M < 0 || F <= 0 || E <= 0 || esize <= 0) return SDMOE_EARG;
+  if (M == 0) return SDMOE_OK;
+  if (F % 8 || ldp % 8 || E * esize != F || ld_score < E) return SDMOE_ESHAPE;
+  if (E > 256) return SDMOE_EUNSUP;
+  if (k < 0 || k > E) return SDMOE_EARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int blocks = (M + 3) / 4;
+  half_t* Pp = (half_t*)P;
+  const half_t* sc = (const half_t*)score;
+  const uint32_t* rm = (const uint32_t*)removed_bits;
+  if (E <= 64) moe_topk_mask_kernel<1><<<blocks, 256, 0, s>>>(Pp, ldp, M, F, E, esize, k, sc, ld_score, rm, sel_out);
+  else if (E <= 128) moe_topk_mask_kernel<2><<<blocks, 256, 0, s>>>(Pp, ldp, M, F, E, esize, k, sc, ld_score, rm, sel_out);
+  else moe_topk_mask_kernel<4><<<blocks, 256, 0, s>>>(Pp, ldp, M, F, E, esize, k, sc, ld_score, rm, sel_out);
+  SDMOE_CHECK_LAUNCH();
+  return SDMOE_OK;
+}
 
 extern "C" int sdmoe_geglu_route(const void* Y, long ldy, int M, int F, int E, int k, int act, const int* labels,
                                  const int* e_off, const int* e_nid, const unsigned* removed_bits, void* out,

@@ -27,6 +27,8 @@ SIGNATURES = {
     "sdmoe_layernorm": [_P, _L, _P, _L, _I, _I, _P, _P, _F, _P],
     "sdmoe_attention": [_P, _L, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _I, _F, _P],
     "sdmoe_geglu_route": [_P, _L, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _L, _P, _L, _P, _P, _P],
+    "sdmoe_linear_geglu": [_P, _L, _P, _L, _P, _P, _L, _I, _I, _I, _I, _P, _L, _I, _P],
+    "sdmoe_moe_topk_mask": [_P, _L, _I, _I, _I, _I, _I, _P, _L, _P, _P, _P],
     "sdmoe_timestep_embedding": [_P, _P, _F, _I, _I, _F, _P],
     "sdmoe_prepare_input": [_P, _P, _I, _I, _L, _I, _P],
     "sdmoe_cfg_ddim_step": [_P, _L, _P, _I, _I, _I, _F, _F, _F, _P, _L, _P],

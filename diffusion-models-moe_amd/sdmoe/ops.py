@@ -212,6 +212,12 @@ class Routing:
         self.labels = labels.to(torch.int32).to(device)
         self.e_off = off.to(torch.int32).to(device)
         self.e_nid = order.to(torch.int32).to(device)
+        # fused path (sdmoe_linear_geglu + sdmoe_moe_topk_mask): balanced experts (the reference's
+        # KMeansConstrained split), permuted expert-major so every expert is a contiguous neuron slice
+        sizes = set(counts.tolist())
+        self.esize = sizes.pop() if len(sizes) == 1 else 0
+        self.perm = order  # new neuron position -> original neuron id (cpu int64)
+        self.fusable = bool(self.esize and 40 % self.esize == 0 and F % 80 == 0 and self.E <= 256)
 
     @classmethod
     def from_patterns(cls, patterns: torch.Tensor, k: int, device=None):
@@ -221,6 +227,50 @@ class Routing:
             raise ValueError("patterns must be a 0/1 [E, F] matrix with exactly one expert per neuron")
         labels = p.argmax(0)
         return cls(labels, E, k, device or patterns.device)
+
+
+def interleave_geglu(weight: torch.Tensor, bias: torch.Tensor | None, perm: torch.Tensor | None):
+    """proj.weight [2F, K] (value rows, then gate rows) -> rows permuted by `perm` and interleaved [v 8 | g 8]
+    per 8 neurons, the layout sdmoe_linear_geglu reads. bias likewise (zeros if None)."""
+    F2, K = weight.shape
+    F = F2 // 2
+    idx = torch.arange(F, device=weight.device) if perm is None else perm.to(weight.device)
+    wv, wg = weight[:F][idx], weight[F:][idx]
+    w_il = torch.stack([wv.view(F // 8, 8, K), wg.view(F // 8, 8, K)], 1).reshape(F2, K).contiguous()
+    b = torch.zeros(F2, dtype=weight.dtype, device=weight.device) if bias is None else bias
+    bv, bg = b[:F][idx], b[F:][idx]
+    b_il = torch.stack([bv.view(F // 8, 8), bg.view(F // 8, 8)], 1).reshape(F2).contiguous()
+    return w_il, b_il
+
+
+def linear_geglu(x, w_il, b_il, act=ACT_GELU, *, score=None, esize=0, out=None):
+    """P = value * act(gate) from the interleaved projection (interleave_geglu), plus per-expert gate sums
+    into score [M, E] (experts = contiguous esize-neuron slices) when given."""
+    lib = _lib.load()
+    xp, lda = _rows(x, "x")
+    M, K = x.shape
+    F = w_il.shape[0] // 2
+    if w_il.shape[1] != K:
+        raise ValueError(f"linear_geglu: weight {tuple(w_il.shape)} does not match input K={K}")
+    if out is None:
+        out = torch.empty((M, F), dtype=torch.float16, device=x.device)
+    op, ldp = _rows(out, "out")
+    sp, lds = (None, 0) if score is None else _rows(score, "score")
+    st = lib.sdmoe_linear_geglu(xp, lda, _dev(w_il, "w"), w_il.stride(0), _dev(b_il, "bias"), op, ldp, M, F, K,
+                                act, sp, lds, int(esize), _stream())
+    _lib.check(st, "sdmoe_linear_geglu")
+    return out
+
+
+def moe_topk_mask(P, score, routing: "Routing", removed=None, sel_out=None):
+    """In place on the fused product P [M, F]: zero the neurons of experts outside each token's top-k."""
+    lib = _lib.load()
+    pp, ldp = _rows(P, "P")
+    sp, lds = _rows(score, "score")
+    st = lib.sdmoe_moe_topk_mask(pp, ldp, P.shape[0], P.shape[1], routing.E, routing.esize, routing.k, sp, lds,
+                                 _ptr(removed), _ptr(sel_out), _stream())
+    _lib.check(st, "sdmoe_moe_topk_mask")
+    return P
 
 
 def removed_bits(expert_ids, num_experts: int, device) -> torch.Tensor:

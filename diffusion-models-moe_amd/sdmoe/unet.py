@@ -25,6 +25,7 @@ from . import ops
 from .config import UNetConfig
 
 CTX_LEN = 77
+FUSED_GEGLU = True  # fused projection+GEGLU(+expert scores) path where eligible (tests flip it for A/B parity)
 IN_PAD = 64    # conv_in input channels padded 4 -> 64 (K-step of the implicit GEMM)
 OUT_PAD = 8    # conv_out output channels padded 4 -> 8 (16-B epilogue stores)
 
@@ -116,6 +117,12 @@ class GEGLU(nn.Module):
         self._routing = None
         self._routing_key = None
         self._sdmoe_deferred = 0
+        # fused projection+GEGLU (+expert scores) path: interleaved/permuted proj weights, and what the last
+        # routed() call produced (its output pointer and permutation) for the FeedForward down projection
+        self._allow_permuted_out = False
+        self._out_perm = None
+        self._il_key = None
+        self._il = None
 
     @property
     def inner_dim(self):
@@ -134,11 +141,39 @@ class GEGLU(nn.Module):
             self._routing_key = key
         return self._routing
 
+    def _interleaved(self, routing):
+        w = self.proj.weight
+        key = (id(routing), w.data_ptr(), w._version,
+               None if self.proj.bias is None else (self.proj.bias.data_ptr(), self.proj.bias._version))
+        if self._il_key != key:
+            perm = routing.perm if routing is not None else None
+            self._il = ops.interleave_geglu(w.data, None if self.proj.bias is None else self.proj.bias.data, perm)
+            self._il_key = key
+        return self._il
+
     def routed(self, x, removed=None, want_gate=False, sel_out=None):
         """proj GEMM + routed GEGLU kernel. x: [..., C] fp16. Returns (out [..., 4C], masked gate or None).
-        sel_out (optional int32 [tokens, ceil(E/32)]) receives the per-token top-k expert bitmask."""
+        sel_out (optional int32 [tokens, ceil(E/32)]) receives the per-token top-k expert bitmask.
+
+        When the caller (FeedForward) allows it and the experts are balanced, the fused path runs instead:
+        the projection GEMM's epilogue computes value*act(gate) and the expert scores, a small kernel applies
+        the top-k mask; `out` is then in the expert-major neuron order (self._out_perm records it)."""
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
+        routing = self.routing()
+        act = act_code(self.gelu)
+        self._out_perm = None
+        if (FUSED_GEGLU and self._allow_permuted_out and not want_gate and self.inner_dim % 80 == 0 and x2.shape[1] % 64 == 0
+                and (routing is None or routing.fusable)):
+            w_il, b_il = self._interleaved(routing)
+            if routing is None:
+                out = ops.linear_geglu(x2, w_il, b_il, act)
+            else:
+                score = torch.empty((x2.shape[0], routing.E), dtype=torch.float16, device=x.device)
+                out = ops.linear_geglu(x2, w_il, b_il, act, score=score, esize=routing.esize)
+                ops.moe_topk_mask(out, score, routing, removed=removed, sel_out=sel_out)
+                self._out_perm = (routing, out.data_ptr())
+            return out.view(*shp[:-1], self.inner_dim), None
         y = self.proj.run(x2)
         gate = torch.empty((x2.shape[0], self.inner_dim), dtype=torch.float16, device=x.device) if want_gate else None
         out = ops.geglu_route(y, self.routing(), act_code(self.gelu), removed=removed, gate_out=gate, sel_out=sel_out)
@@ -155,14 +190,33 @@ class FeedForward(nn.Module):
     def __init__(self, geglu, down):
         super().__init__()
         self.net = nn.ModuleList([geglu, nn.Dropout(0.0), down])
+        self._wperm_key = None
+        self._wperm = None
+
+    def _down_weight_permuted(self, routing):
+        w = self.net[2].weight
+        key = (id(routing), w.data_ptr(), w._version)
+        if self._wperm_key != key:
+            self._wperm = w.data[:, routing.perm.to(w.device)].contiguous()
+            self._wperm_key = key
+        return self._wperm
 
     def run(self, x2d, nimg, residual):
         geglu, down = self.net[0], self.net[2]
-        h = geglu(x2d.view(nimg, -1, x2d.shape[1]))
+        # a hook on the down projection (Wanda weight masks) sees the natural neuron order
+        geglu._allow_permuted_out = not down._forward_hooks
+        try:
+            h = geglu(x2d.view(nimg, -1, x2d.shape[1]))
+        finally:
+            geglu._allow_permuted_out = False
         if down._forward_hooks:
             o = down(h)
             return ops.add(o.reshape(residual.shape).contiguous(), residual)
-        return down.run(h.reshape(-1, h.shape[-1]), residual=residual)
+        h2 = h.reshape(-1, h.shape[-1])
+        perm = geglu._out_perm
+        if perm is not None and perm[1] == h2.data_ptr():
+            return ops.linear(h2, self._down_weight_permuted(perm[0]), down.bias, residual=residual)
+        return down.run(h2, residual=residual)
 
 
 class Attention(nn.Module):

@@ -103,6 +103,25 @@ int sdmoe_geglu_route(const void* Y, long ldy, int M, int F, int E, int k, int a
                       const int* e_off, const int* e_nid, const unsigned* removed_bits, void* out, long ldo,
                       void* gate_out, long ldg, unsigned* sel_out, void* score_out, void* stream);
 
+/*
+ * Fused form of the same routing for balanced experts (the reference's KMeansConstrained split: every expert
+ * has esize neurons, esize | 40), in two launches and without the [M, 2F] projection output:
+ *  1. sdmoe_linear_geglu: P[m, n] = fp16(fp16(x W_v^T + b_v) * fp16(act(fp16(x W_g^T + b_g)))) for all F neurons
+ *     and score[m, e] = fp16(sum over expert e's neurons of act(gate)) in the GEMM epilogue. W [2F, K] / bias
+ *     [2F] hold the neurons permuted so every expert is contiguous (expert-major, ascending neuron id), value
+ *     and gate rows interleaved in chunks of 8 ([v 8 | g 8] per 8 neurons). F % 80 == 0. score may be NULL
+ *     (dense GEGLU). Same rounding points as sdmoe_linear + sdmoe_geglu_route.
+ *  2. sdmoe_moe_topk_mask: per token, removed experts score 0, top-k (ties toward the lowest expert id) and
+ *     zero every neuron of P whose expert is not selected or removed. sel_out as above (may be NULL).
+ * The permuted P feeds the down projection with W_down's columns permuted the same way.
+ * Replaces: the same reference hooks as sdmoe_geglu_route (moefy.py:10-27, remove_skilled_experts.py:24-55),
+ * with SURVEY §3 K1+K2+K3 fused into the projection GEMM.
+ */
+int sdmoe_linear_geglu(const void* A, long lda, const void* W, long ldw, const void* bias, void* P, long ldp,
+                       int M, int F, int K, int act, void* score, long ld_score, int esize, void* stream);
+int sdmoe_moe_topk_mask(void* P, long ldp, int M, int F, int E, int esize, int k, const void* score,
+                        long ld_score, const unsigned* removed_bits, unsigned* sel_out, void* stream);
+
 /* diffusers get_timestep_embedding for one timestep (t_dev if non-NULL, else t), fp16 [dim]. */
 int sdmoe_timestep_embedding(void* out, const float* t_dev, float t, int dim, int flip_sin_to_cos, float freq_shift,
                              void* stream);

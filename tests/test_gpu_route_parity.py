@@ -155,3 +155,77 @@ def test_full_hook_vs_reference(name, c):
     sc = score.float().cpu().numpy()
     ours[np.arange(sc.shape[0])[:, None], np.argsort(-sc, axis=1, kind="stable")[:, :k]] = True
     assert (ours[clear] == ref_sel[clear]).all()
+
+
+# ---- fused path: proj GEMM epilogue (value*act(gate) + expert scores) + top-k mask kernel -----------------
+
+def _fused(x, w, b, routing, act, removed=None):
+    w_il, b_il = ops.interleave_geglu(w, b, routing.perm)
+    score = torch.empty((x.shape[0], routing.E), dtype=torch.float16, device=DEV)
+    sel = torch.zeros((x.shape[0], (routing.E + 31) // 32), dtype=torch.int32, device=DEV)
+    P = ops.linear_geglu(x, w_il, b_il, act, score=score, esize=routing.esize)
+    ops.moe_topk_mask(P, score, routing, removed=removed, sel_out=sel)
+    out = torch.empty_like(P)
+    out[:, routing.perm.to(DEV)] = P  # back to the natural neuron order
+    return out, score, sel
+
+
+@pytest.mark.parametrize("M,C,E,k,act,nrem", [(4096, 320, 64, 12, ops.ACT_GELU, 0), (1000, 320, 64, 12, ops.ACT_RELU, 5),
+                                              (2048, 640, 128, 25, ops.ACT_GELU, 9), (512, 1280, 256, 51, ops.ACT_GELU, 20),
+                                              (333, 640, 128, 128, ops.ACT_RELU, 0)])
+def test_fused_geglu_bit_exact_vs_unfused(M, C, E, k, act, nrem):
+    """Same rounding points and the same neuron-order fp32 score sums as proj GEMM + sdmoe_geglu_route:
+    output, scores and top-k bits are bit-identical (no split-K at K = C, so the GEMM sums agree too)."""
+    g = torch.Generator().manual_seed(M + C)
+    F = 4 * C
+    x = (torch.randn(M, C, generator=g)).half().to(DEV)
+    w = (torch.randn(2 * F, C, generator=g) * C ** -0.5).half().to(DEV)
+    b = (torch.randn(2 * F, generator=g) * 0.3).half().to(DEV)
+    labels = torch.randperm(F, generator=g) % E  # balanced, scattered over the neurons
+    routing = ops.Routing(labels, E, k, DEV)
+    assert routing.fusable and routing.esize == F // E
+    removed = ops.removed_bits(torch.randperm(E, generator=g)[:nrem].tolist(), E, DEV) if nrem else None
+    out, score, sel = _fused(x, w, b, routing, act, removed)
+    y = ops.linear(x, w, b)
+    score_u = torch.empty_like(score)
+    sel_u = torch.zeros_like(sel)
+    out_u = ops.geglu_route(y, routing, act, removed=removed, sel_out=sel_u, score_out=score_u)
+    if removed is not None:  # the unfused kernel reports removed experts' scores as 0; fused reports raw sums
+        rm = sel_bits_to_bool(removed.view(1, -1).expand(M, -1).contiguous(), E)
+        score = score.masked_fill(torch.from_numpy(rm).to(DEV), 0)
+    assert torch.equal(score, score_u)
+    assert torch.equal(sel, sel_u)
+    assert torch.equal(out, out_u)
+
+
+def test_fused_geglu_dense_matches_unfused():
+    M, C = 1500, 320
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(M, C, generator=g).half().to(DEV)
+    w = (torch.randn(8 * C, C, generator=g) * C ** -0.5).half().to(DEV)
+    b = (torch.randn(8 * C, generator=g) * 0.3).half().to(DEV)
+    w_il, b_il = ops.interleave_geglu(w, b, None)
+    assert torch.equal(ops.linear_geglu(x, w_il, b_il, ops.ACT_GELU), ops.geglu_route(ops.linear(x, w, b), None))
+
+
+@pytest.mark.parametrize("name,c", cases({"moefy"}), ids=[n for n, _ in cases({"moefy"})])
+def test_fused_hook_vs_reference(name, c):
+    """The fused path on the reference's inputs vs the reference hook output (same bar as the unfused path)."""
+    C, E, k = int(c["C"]), int(c["E"]), int(c["k"])
+    w, b = synth.geglu_weights(C, int(c["seed"]))
+    x = torch.from_numpy(c["x"]).reshape(-1, C).to(DEV)
+    routing = ops.Routing(torch.from_numpy(c["labels"]), E, k, DEV)
+    assert routing.fusable
+    out, score, sel = _fused(x, torch.from_numpy(w).half().to(DEV), torch.from_numpy(b).half().to(DEV), routing,
+                             act_code(c["act"]))
+    ref = c["out"].reshape(-1, 4 * C).astype(np.float32)
+    s = np.sort(c["score"].astype(np.float32), axis=1)[:, ::-1]
+    gap = s[:, k - 1] - s[:, k] if k < E else np.full(s.shape[0], np.inf)
+    clear = gap > 8 * fp16_spacing(s[:, min(k, E - 1)])
+    o = out.float().cpu().numpy()
+    err = np.abs(o[clear] - ref[clear]).max() if clear.any() else 0.0
+    assert err <= 2e-2 * max(1.0, np.abs(ref).max())
+    ref_sel = np.zeros((x.shape[0], E), dtype=bool)
+    np.put_along_axis(ref_sel, c["sel"].reshape(x.shape[0], -1), True, axis=1)
+    ours = sel_bits_to_bool(sel, E)
+    assert (ours[clear] == ref_sel[clear]).all()

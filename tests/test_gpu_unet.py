@@ -297,3 +297,50 @@ def test_pipeline_wanda_union_receiver_tiny(tiny):
         return hook
     exp = run_oracle(ref, cfg, ["a parachute over a church"], 2, down_hook_factory=down_factory)
     assert rel_l2(out, exp[0]) <= 3e-2
+
+
+@pytest.mark.parametrize("receiver", ["moefy", "remove"])
+def test_pipeline_fused_geglu_sd14(receiver):
+    """SD-1.4 widths (F = 1280/2560/5120, balanced 20-neuron experts): fused projection+GEGLU+score path vs
+    the unfused proj GEMM + route kernel. Per call the two are bit-identical (test_gpu_route_parity); the down
+    projection then sums the permuted neurons in another fp32 order, so with top-k = all experts (no
+    near-tie can flip a choice) one U-Net evaluation agrees to rel L2 <= 2e-3 and a 2-step CFG 7.5 pipeline
+    (which amplifies fp16 noise ~7.5x per step) to <= 2e-2. The removal variant zeroes fixed experts,
+    exercising the removed-bit path through the permutation."""
+    from moefication.helper import moefy_synthetic
+    from neuron_receivers import MOEFy, RemoveExperts
+    import sdmoe.unet as U
+    cfg = UNetConfig.sd14(16)
+    unet = UNet2DConditionModel.from_state_dict(make_state_dict(cfg, 4), cfg, DEV)
+    pipe = StableDiffusionPipeline(unet, DEV, num_inference_steps=2)
+    moefy_synthetic(pipe, 1.0, 20, seed=1)
+    if receiver == "moefy":
+        make = lambda: MOEFy(seed=0, store_gates=False)  # noqa: E731
+    else:
+        lists = {t: {l: list(range(l % 5, 64, 7)) for l in range(16)} for t in range(51)}
+        make = lambda: RemoveExperts(0, None, T=51, n_layers=16, store_gates=False,  # noqa: E731
+                                     expert_indices=lists)
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(2, 4, 16, 16, generator=g).to(DEV)
+    ctx = ctx_for(cfg, ["Starry night by Van Gogh"]).to(DEV)
+    evals, outs = [], []
+    for fused in (True, False):
+        U.FUSED_GEGLU = fused
+        try:
+            rec = make()
+            if hasattr(rec, "prepare"):
+                rec.prepare(pipe)
+            hooks = rec.register_hooks(pipe)
+            try:
+                evals.append(unet(x, 741.0, ctx))
+            finally:
+                rec.remove_hooks(hooks)
+            out, _ = make().observe_activation(pipe, ["a cat", "Starry night by Van Gogh"])
+        finally:
+            U.FUSED_GEGLU = True
+        outs.append(torch.stack(out))
+    assert torch.isfinite(outs[0]).all()
+    assert rel_l2(evals[0], evals[1]) <= 2e-3
+    assert rel_l2(outs[0], outs[1]) <= 2e-2
+    ffs = [m for n, m in unet.named_modules() if n.endswith(".ff")]
+    assert ffs and all(f._wperm is not None for f in ffs)  # the fused path actually ran
