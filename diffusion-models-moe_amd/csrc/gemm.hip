@@ -25,6 +25,8 @@ constexpr int BK = 64;
 // tuning knobs (sdmoe_tune): 0 = LDS stages (0 = auto, 2 or 3); 1 = forced tile config (0 = auto)
 int g_stages = 0;
 int g_tile = 0;
+int g_bk = 0;
+int g_prio = 0;
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
@@ -46,9 +48,9 @@ struct GemmParams {
   // routed-GEGLU epilogue (sdmoe_linear_geglu): W rows interleaved [value 8 | gate 8] per 8-neuron chunk, C is
   // the [M, N/2] product value * act(gate); score [M, ld_score] gets per-expert sums of act(gate) over
   // contiguous esize-neuron experts (neurons pre-permuted so every expert is contiguous)
-  int geglu;
   half_t* score; long ld_score;
   int esize;
+  int prio;  // experiment knob: raise wave priority around the MFMA block
 };
 
 SDMOE_DEV int swz(int row) { return (row >> 1) & 7; }
@@ -87,53 +89,100 @@ SDMOE_DEV void epilogue8(const GemmParams& p, int m, int n, float (&v)[8]) {
   *reinterpret_cast<half8*>(p.C + (long)m * p.ldc + n) = o;
 }
 
-enum { MODE_GEMM = 0, MODE_CONV = 1, MODE_CONV_UP = 2 };
+enum { MODE_GEMM = 0, MODE_CONV = 1, MODE_CONV_UP = 2, MODE_GEGLU = 3 };  // GEGLU: GEMM loads, routed-GEGLU epilogue
 
 // Routed-GEGLU epilogue over one staged pass (rows x WN fp32 in LDS, row stride WN_PAD) of a wave's tile
 // whose columns n0..n0+WN-1 are [value 8 | gate 8] chunk pairs. Rounds exactly like the unfused path
 // (fp16 linear output, fp16 act, fp16 product; expert score = fp32 sum in neuron order, rounded to fp16).
-template <int WN, int WN_PAD>
-SDMOE_DEV void geglu_pass(const GemmParams& p, const float* st, int mrow0, int rows, int n0, int lane) {
-  constexpr int PPR = WN / 16;  // chunk pairs per row
-  for (int id = lane; id < rows * PPR; id += 64) {
-    const int r = id / PPR, j = id - r * PPR;
-    const int m = mrow0 + r, n = n0 + 16 * j;
-    if (m >= p.M) continue;
-    const float* sp = st + r * WN_PAD + 16 * j;
-    const half8 bh = *reinterpret_cast<const half8*>(p.bias + n);
-    const half8 bg = *reinterpret_cast<const half8*>(p.bias + n + 8);
-    half8 o;
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const half_t yh = (half_t)(sp[t] + (float)bh[t]);
-      const half_t ga = (half_t)apply_act((float)(half_t)(sp[8 + t] + (float)bg[t]), p.act);
-      o[t] = (half_t)((float)yh * (float)ga);
-    }
-    *reinterpret_cast<half8*>(p.C + (long)m * p.ldc + n / 2) = o;
-  }
-  if (!p.score) return;
-  const int S = p.esize, NE = (WN / 2) / S;
+template <int S, int WN, int WN_PAD>
+SDMOE_DEV void expert_sums(const GemmParams& p, const float* st, int mrow0, int rows, int n0, int lane) {
+  constexpr int NE = (WN / 2) / S;
   for (int id = lane; id < rows * NE; id += 64) {
     const int r = id / NE, e = id - r * NE;
     const int m = mrow0 + r;
-    if (m >= p.M) continue;
+    const float* rp = st + r * WN_PAD + 8;
+    float v[S];
+#pragma unroll
+    for (int t = 0; t < S; ++t) v[t] = rp[16 * ((e * S + t) >> 3) + ((e * S + t) & 7)];
     float acc = 0.f;
-    for (int t = e * S; t < (e + 1) * S; ++t) {
-      const int col = 16 * (t >> 3) + 8 + (t & 7);
-      acc += (float)(half_t)apply_act((float)(half_t)(st[r * WN_PAD + col] + (float)p.bias[n0 + col]), p.act);
-    }
-    p.score[(long)m * p.ld_score + n0 / 2 / S + e] = (half_t)acc;
+#pragma unroll
+    for (int t = 0; t < S; ++t) acc += v[t];  // neuron order, as the unfused kernel
+    if (m < p.M) p.score[(long)m * p.ld_score + n0 / 2 / S + e] = (half_t)acc;
   }
 }
 
-template <int BM, int BN, int WMW, int WNW, int MODE, int NSTAGE>
+// bias of this lane's chunk pairs (the same in every pass): up to GB iterations of the id loop below
+template <int WN, int WN_PAD, int ROWS>
+SDMOE_DEV void geglu_pass(const GemmParams& p, float* st, int mrow0, int n0, int lane, const float* gbias) {
+  constexpr int PPR = WN / 16;  // chunk pairs per row
+  constexpr int rows = ROWS;
+  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+  for (int it = 0; it < (ROWS * PPR + 63) / 64; ++it) {
+    const int id = lane + 64 * it;
+    if (id >= rows * PPR) break;
+    const int r = id / PPR, j = id - r * PPR;
+    const int m = mrow0 + r, n = n0 + 16 * j;
+    float* sp = st + r * WN_PAD + 16 * j;
+    const float* bp = gbias + 16 * j;
+    // fp16 linear outputs (fp32 acc + bias, rounded once), then act / product on packed halves: the product of
+    // two fp16 values is exact in fp32, so the packed fp16 multiply rounds identically
+    h2 yh[4], yg[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      yh[t] = (h2){(half_t)(sp[2 * t] + bp[2 * t]), (half_t)(sp[2 * t + 1] + bp[2 * t + 1])};
+      yg[t] = (h2){(half_t)(sp[8 + 2 * t] + bp[8 + 2 * t]), (half_t)(sp[9 + 2 * t] + bp[9 + 2 * t])};
+    }
+    h2 ga[4];
+    if (p.act == ACT_RELU) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) ga[t] = __builtin_elementwise_max(yg[t], (h2){(half_t)0.f, (half_t)0.f});
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        ga[t] = (h2){(half_t)apply_act((float)yg[t][0], p.act), (half_t)apply_act((float)yg[t][1], p.act)};
+    }
+    half8 o;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const h2 pr = yh[t] * ga[t];
+      o[2 * t] = pr[0];
+      o[2 * t + 1] = pr[1];
+    }
+    // the activated gate, for the expert sums
+    *reinterpret_cast<float4v*>(sp + 8) = (float4v){(float)ga[0][0], (float)ga[0][1], (float)ga[1][0], (float)ga[1][1]};
+    *reinterpret_cast<float4v*>(sp + 12) = (float4v){(float)ga[2][0], (float)ga[2][1], (float)ga[3][0], (float)ga[3][1]};
+    if (m < p.M) *reinterpret_cast<half8*>(p.C + (long)m * p.ldc + n / 2) = o;
+  }
+  if (!p.score) return;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  switch (p.esize) {
+    case 20: expert_sums<20, WN, WN_PAD>(p, st, mrow0, rows, n0, lane); break;
+    case 10: expert_sums<10, WN, WN_PAD>(p, st, mrow0, rows, n0, lane); break;
+    case 40: expert_sums<40, WN, WN_PAD>(p, st, mrow0, rows, n0, lane); break;
+    case 8: expert_sums<8, WN, WN_PAD>(p, st, mrow0, rows, n0, lane); break;
+    case 5: expert_sums<5, WN, WN_PAD>(p, st, mrow0, rows, n0, lane); break;
+    case 4: expert_sums<4, WN, WN_PAD>(p, st, mrow0, rows, n0, lane); break;
+    case 2: expert_sums<2, WN, WN_PAD>(p, st, mrow0, rows, n0, lane); break;
+    default: expert_sums<1, WN, WN_PAD>(p, st, mrow0, rows, n0, lane); break;
+  }
+}
+
+template <int BM, int BN, int WMW, int WNW, int MODE, int NSTAGE, int BKT>
 __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 : 1)) void gemm_kernel(GemmParams p) {
-  constexpr bool CONV = MODE != MODE_GEMM;
+  constexpr int BK = BKT;                        // K per stage: 64 (128-B rows) or 32 (64-B rows, deeper ring)
+  constexpr int RB = BK * 2, CPRW = BK / 8;      // LDS row bytes, 16-B chunks per row
+  constexpr int RPP = 1024 / RB;                 // rows per 1-KiB LDS-DMA piece
+  auto swzk = [](int row) { return (row >> 1) & (CPRW - 1); };  // conflict-free b128 fragment reads
+  constexpr bool CONV = MODE == MODE_CONV || MODE == MODE_CONV_UP;
+  constexpr bool GEGLU = MODE == MODE_GEGLU;
   constexpr int NW = WMW * WNW;                  // waves per workgroup
   constexpr int WM = BM / WMW, WN = BN / WNW;    // per-wave output tile
   constexpr int FM = WM / 16, FN = WN / 16;
   static_assert(WM % 16 == 0 && WN % 16 == 0, "wave tile must be whole 16x16 fragments");
-  constexpr int A_INS = BM / 8, B_INS = BN / 8;  // 1-KiB LDS-DMA wave-instructions (8 rows) per stage
+  constexpr int A_INS = BM / RPP, B_INS = BN / RPP;  // 1-KiB LDS-DMA wave-instructions per stage
   constexpr int A_PW = (A_INS + NW - 1) / NW, B_PW = (B_INS + NW - 1) / NW;
   constexpr int PER_WAVE = A_PW + B_PW;          // every wave issues exactly this many (surplus -> dummy slot)
   constexpr int STAGE_AB = (BM + BN) * BK * 2;
@@ -163,7 +212,7 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
   // hardware range check and lands as zeros, which gives conv halo rows and M/N tails for free.
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsW = __builtin_amdgcn_make_buffer_rsrc((void*)p.W, (short)0, p.w_bytes, 0x00020000);
-  const int lrow = lane >> 3, lch = lane & 7;
+  const int lrow = lane / CPRW, lch = lane % CPRW;
   // A rows: wave w stages rows [8*(w*A_PW + j), +8); B rows likewise with B_PW
   unsigned avoff[A_PW];  // GEMM: byte offset of (row, pre-swizzled chunk); conv: of the centre-tap pixel
   unsigned amask[A_PW];  // conv: bit t = tap t in bounds (0 = M-tail row)
@@ -171,12 +220,12 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
   unsigned bvoff[B_PW];
 #pragma unroll
   for (int j = 0; j < A_PW; ++j) {
-    const int r = 8 * (j * NW + wave) + lrow;
-    const unsigned chb = (unsigned)((lch ^ swz(r)) * 16);
+    const int r = RPP * (j * NW + wave) + lrow;
+    const unsigned chb = (unsigned)((lch ^ swzk(r)) * 16);
     const int m = m0 + r;
     avoff[j] = OOB; amask[j] = 0; aoh[j] = 0; aow[j] = 0; ab_[j] = 0;
     if (j * NW + wave < A_INS && m < p.M) {
-      if (MODE == MODE_GEMM) {
+      if (!CONV) {
         avoff[j] = (unsigned)((long)m * p.lda * 2) + chb;
       } else {
         const int hw = p.OH * p.OW;
@@ -200,9 +249,9 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
   }
 #pragma unroll
   for (int j = 0; j < B_PW; ++j) {
-    const int r = 8 * (j * NW + wave) + lrow;
+    const int r = RPP * (j * NW + wave) + lrow;
     const int n = n0 + r;
-    bvoff[j] = (j * NW + wave < B_INS && n < p.N) ? (unsigned)((long)n * p.ldw * 2) + (unsigned)((lch ^ swz(r)) * 16)
+    bvoff[j] = (j * NW + wave < B_INS && n < p.N) ? (unsigned)((long)n * p.ldw * 2) + (unsigned)((lch ^ swzk(r)) * 16)
                                                   : OOB;
   }
   // LDS destination of wave-instruction j (surplus instructions of a padded tile land in a dummy 1-KiB slot)
@@ -216,7 +265,7 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
   auto issue_stage = [&](int ks, int buf) {
     char* sa = smem + buf * STAGE;
     const unsigned kb = (unsigned)(ks * BK * 2);
-    if (MODE == MODE_GEMM) {
+    if (!CONV) {
 #pragma unroll
       for (int j = 0; j < A_PW; ++j) bld16(rsA, sa + a_dst(j), avoff[j], kb);
     } else {
@@ -261,33 +310,44 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
 
   const int fr = lane & 15, fg = lane >> 4;
   for (int it = 0; it < nk; ++it) {
-    // wait for this K-step's tile (leave the next one in flight), then make every wave's DMA visible
-    if (NSTAGE == 3 && it + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_WAVE) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // wait for this K-step's tile (leave the later ones in flight), then make every wave's DMA visible
+    {
+      const int ahead = min(NSTAGE - 2, nk - 1 - it);  // stages issued after this one (wave-uniform)
+      if (NSTAGE >= 4 && ahead >= 2) {
+        if (NSTAGE >= 5 && ahead >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * PER_WAVE) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER_WAVE) : "memory");
+      } else if (NSTAGE >= 3 && ahead >= 1) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_WAVE) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (it + NSTAGE - 1 < nk) issue_stage(ks0 + it + NSTAGE - 1, (it + NSTAGE - 1) % NSTAGE);
 
     const char* sa = smem + (it % NSTAGE) * STAGE;
     const char* sbm = sa + BM * BK * 2;
+    if (p.prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    for (int kk = 0; kk < BK / 32; ++kk) {
       half8 af[FM], bf[FN];
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int row = wr * WM + i * 16 + fr;
-        af[i] = *reinterpret_cast<const half8*>(sa + row * 128 + (((kk * 4 + fg) ^ swz(row)) << 4));
+        af[i] = *reinterpret_cast<const half8*>(sa + row * RB + (((kk * 4 + fg) ^ swzk(row)) << 4));
       }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int row = wc * WN + j * 16 + fr;
-        bf[j] = *reinterpret_cast<const half8*>(sbm + row * 128 + (((kk * 4 + fg) ^ swz(row)) << 4));
+        bf[j] = *reinterpret_cast<const half8*>(sbm + row * RB + (((kk * 4 + fg) ^ swzk(row)) << 4));
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32(af[i], bf[j], acc[i][j]);
     }
+    if (p.prio) __builtin_amdgcn_s_setprio(0);
   }
 
   // ---- epilogue: per wave, stage half of its fp32 tile (FM/2 fragment rows) in LDS at a time, then write
@@ -295,6 +355,12 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   float* st = reinterpret_cast<float*>(smem) + wave * (WM / NPASS) * WN_PAD;
+  // GEGLU: this wave's WN bias values (fp32) copied once into LDS past the staging area (per wave, no block sync)
+  float* gbias = reinterpret_cast<float*>(smem + EPI) + wave * WN;
+  if constexpr (GEGLU) {
+    static_assert(EPI + NW * WN * 4 <= SMEM, "GEGLU bias slot must fit behind the epilogue staging");
+    for (int c = lane; c < WN; c += 64) gbias[c] = (float)p.bias[n0 + wc * WN + c];
+  }
   constexpr int CPR = WN / 8;
 #pragma unroll
   for (int h = 0; h < NPASS; ++h) {
@@ -307,8 +373,8 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (p.geglu) {
-      geglu_pass<WN, WN_PAD>(p, st, m0 + wr * WM + h * (WM / NPASS), WM / NPASS, n0 + wc * WN, lane);
+    if constexpr (GEGLU) {
+      geglu_pass<WN, WN_PAD, WM / NPASS>(p, st, m0 + wr * WM + h * (WM / NPASS), n0 + wc * WN, lane, gbias);
     } else
     for (int id = lane; id < (WM / NPASS) * CPR; id += 64) {
       const int r = id / CPR, c8 = id - r * CPR;
@@ -350,7 +416,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
 template <int BM, int BN, int WMW, int WNW, int MODE>
 int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
   const int ntiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-  const int nk = p.K / BK;
+  const int nk = p.K / 64;
   int ksplit = 1;
   // fill the chip: split K when the tile grid covers well under one wave of 256 CUs
   if (ws && ntiles < 192 && nk >= 16) {
@@ -360,20 +426,24 @@ int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
     while (ksplit > 1 && (long)ksplit * p.M * p.N > ws_floats) --ksplit;
   }
   p.ksplit = ksplit > 1 ? ksplit : 1;
+  constexpr int NT = 64 * WMW * WNW;
   p.kchunk = (nk + p.ksplit - 1) / p.ksplit;
   p.part = p.ksplit > 1 ? ws : nullptr;
-  constexpr int NT = 64 * WMW * WNW;
-  // 4-wave tiles: 2-stage ring (2 workgroups/CU, latency hidden across workgroups) when the grid has >= ~300
-  // workgroups, else 3-stage (1 workgroup/CU, two K-steps in flight) -- measured crossover on MI355X.
-  // 8-wave tiles run one workgroup per CU either way: 3-stage where it fits in LDS (256x160), else 2-stage.
-  int stages = g_stages ? g_stages : ((WMW * WNW == 4 && ntiles * p.ksplit >= 300) ? 2 : 3);
-  constexpr bool FITS3 = 3 * ((BM + BN) * BK * 2 + 1024) <= 160 * 1024;
-  if constexpr (FITS3) {
-    if (stages == 2) gemm_kernel<BM, BN, WMW, WNW, MODE, 2><<<ntiles * p.ksplit, NT, 0, s>>>(p);
-    else gemm_kernel<BM, BN, WMW, WNW, MODE, 3><<<ntiles * p.ksplit, NT, 0, s>>>(p);
-  } else {
-    (void)stages;
-    gemm_kernel<BM, BN, WMW, WNW, MODE, 2><<<ntiles * p.ksplit, NT, 0, s>>>(p);
+  p.prio = g_prio;
+  const dim3 grid(ntiles * p.ksplit);
+  {
+    // 64-deep K-steps (a 32-deep 4/5-stage ring measured slower on every shape; the kernel is generic in BK).
+    // 4-wave tiles: 2-stage ring (2 workgroups/CU) when the grid has >= ~300 workgroups, else 3-stage; 8-wave
+    // tiles: 3-stage where it fits in LDS -- measured crossovers on MI355X.
+    const int stages = g_stages ? g_stages : ((WMW * WNW == 4 && ntiles * p.ksplit >= 300) ? 2 : 3);
+    constexpr bool FITS3 = 3 * ((BM + BN) * 64 * 2 + 1024) <= 160 * 1024;
+    if constexpr (FITS3) {
+      if (stages == 2) gemm_kernel<BM, BN, WMW, WNW, MODE, 2, 64><<<grid, NT, 0, s>>>(p);
+      else gemm_kernel<BM, BN, WMW, WNW, MODE, 3, 64><<<grid, NT, 0, s>>>(p);
+    } else {
+      (void)stages;
+      gemm_kernel<BM, BN, WMW, WNW, MODE, 2, 64><<<grid, NT, 0, s>>>(p);
+    }
   }
   SDMOE_CHECK_LAUNCH();
   if (p.ksplit > 1) {
@@ -390,9 +460,12 @@ int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
 int dispatch_geglu(const GemmParams& p, hipStream_t s) {
   const int nt320 = ((p.M + 255) / 256) * (p.N / 320);
   const int nt160_128 = ((p.M + 127) / 128) * (p.N / 160);
-  if (p.N % 320 == 0 && nt320 >= 240) return launch_tile<256, 320, 2, 4, MODE_GEMM>(p, nullptr, 0, s);
-  if (nt160_128 >= 200 || p.M > 2048) return launch_tile<128, 160, 2, 2, MODE_GEMM>(p, nullptr, 0, s);
-  return launch_tile<64, 160, 2, 2, MODE_GEMM>(p, nullptr, 0, s);
+  if (p.N % 320 == 0 && nt320 >= 240) {
+    if (g_tile == 3) return launch_tile<256, 320, 2, 4, MODE_GEGLU>(p, nullptr, 0, s);
+    return launch_tile<256, 320, 4, 2, MODE_GEGLU>(p, nullptr, 0, s);  // wave rows of 160 B: 32-B aligned stores
+  }
+  if (nt160_128 >= 200 || p.M > 2048) return launch_tile<128, 160, 2, 2, MODE_GEGLU>(p, nullptr, 0, s);
+  return launch_tile<64, 160, 2, 2, MODE_GEGLU>(p, nullptr, 0, s);
 }
 
 template <int MODE>
@@ -403,6 +476,7 @@ int dispatch(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
   if (g_tile == 2) return launch_tile<64, 160, 2, 2, MODE>(p, ws, ws_floats, s);
   if (g_tile == 3 && p.N % 320 == 0) return launch_tile<256, 320, 2, 4, MODE>(p, ws, ws_floats, s);
   if (g_tile == 4 && p.N % 160 == 0) return launch_tile<256, 160, 4, 2, MODE>(p, ws, ws_floats, s);
+  if (g_tile == 5 && p.N % 320 == 0) return launch_tile<256, 320, 4, 2, MODE>(p, ws, ws_floats, s);
   // 8-wave 256x320 tile (wave tile 128x80: 2.5x the MFMA work per LDS byte of 64x80) whenever it alone fills
   // the chip; 256x160 8-wave + split-K for long-K problems whose 128x160 grid is under ~1.2 waves of CUs.
   // Measured on MI355X with tools/gemm_bench.py --tile.
@@ -507,7 +581,7 @@ extern "C" int sdmoe_linear_geglu(const void* A, long lda, const void* W, long l
   p.A = (const half_t*)A; p.lda = lda; p.W = (const half_t*)W; p.ldw = ldw;
   p.bias = (const half_t*)bias; p.C = (half_t*)P; p.ldc = ldp;
   p.M = M; p.N = 2 * F; p.K = K; p.act = act; p.rows_per_batch = 1;
-  p.geglu = 1; p.score = (half_t*)score; p.ld_score = ld_score; p.esize = esize;
+  p.score = (half_t*)score; p.ld_score = ld_score; p.esize = esize;
   const long ab = ((long)(M - 1) * lda + K) * 2, wb = ((long)(2 * F - 1) * ldw + K) * 2;
   if (ab >= (long)OOB || wb >= (long)OOB) return SDMOE_ESHAPE;
   p.a_bytes = (int)ab; p.w_bytes = (int)wb;
@@ -561,6 +635,8 @@ extern "C" int sdmoe_mask_weight(const void* W, const void* bits, long N, long K
 
 extern "C" int sdmoe_tune(int knob, int value) {
   if (knob == 0 && (value == 0 || value == 2 || value == 3)) { g_stages = value; return SDMOE_OK; }
-  if (knob == 1 && value >= 0 && value <= 4) { g_tile = value; return SDMOE_OK; }
+  if (knob == 1 && value >= 0 && value <= 5) { g_tile = value; return SDMOE_OK; }
+  if (knob == 2 && (value == 0 || value == 32 || value == 64)) { g_bk = value; return SDMOE_OK; }
+  if (knob == 3 && (value == 0 || value == 1)) { g_prio = value; return SDMOE_OK; }
   return SDMOE_EARG;
 }

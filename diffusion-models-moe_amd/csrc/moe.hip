@@ -143,14 +143,15 @@ __global__ __launch_bounds__(256) void geglu_route_kernel(RouteParams p) {
 // Top-k expert mask over a routed-GEGLU product computed by sdmoe_linear_geglu (experts contiguous, esize
 // neurons each): per token, scores (fp16, removed experts -> 0) -> the same radix top-k as above -> zero the
 // neurons of every expert that is not selected (or is removed). One wave per token; only zeros are written.
-template <int SLOTS>
+template <int SLOTS, int SC>  // SC: compile-time expert size (0 = runtime S)
 __global__ __launch_bounds__(256) void moe_topk_mask_kernel(half_t* __restrict__ P, long ldp, int M, int F, int E,
-                                                            int S, int k, const half_t* __restrict__ score,
+                                                            int S_, int k, const half_t* __restrict__ score,
                                                             long lds, const uint32_t* __restrict__ removed,
                                                             uint32_t* __restrict__ sel_out) {
   __shared__ uint32_t selw_all[4][8];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t* selw = selw_all[wave];
+  const int S = SC ? SC : S_;
   const int m = blockIdx.x * 4 + wave;
   if (m >= M) return;  // wave-uniform; no block-level barrier below
   const int nw = (E + 31) >> 5;
@@ -231,9 +232,18 @@ extern "C" int sdmoe_moe_topk_mask(void* P, long ldp, int M, int F, int E, int e
   half_t* Pp = (half_t*)P;
   const half_t* sc = (const half_t*)score;
   const uint32_t* rm = (const uint32_t*)removed_bits;
-  if (E <= 64) moe_topk_mask_kernel<1><<<blocks, 256, 0, s>>>(Pp, ldp, M, F, E, esize, k, sc, ld_score, rm, sel_out);
-  else if (E <= 128) moe_topk_mask_kernel<2><<<blocks, 256, 0, s>>>(Pp, ldp, M, F, E, esize, k, sc, ld_score, rm, sel_out);
-  else moe_topk_mask_kernel<4><<<blocks, 256, 0, s>>>(Pp, ldp, M, F, E, esize, k, sc, ld_score, rm, sel_out);
+#define SDMOE_TOPK_MASK(SL, SC) \
+  moe_topk_mask_kernel<SL, SC><<<blocks, 256, 0, s>>>(Pp, ldp, M, F, E, esize, k, sc, ld_score, rm, sel_out)
+  if (esize == 20) {  // the reference's expert size (KMeansConstrained, 20 neurons): divisions by a constant
+    if (E <= 64) SDMOE_TOPK_MASK(1, 20);
+    else if (E <= 128) SDMOE_TOPK_MASK(2, 20);
+    else SDMOE_TOPK_MASK(4, 20);
+  } else {
+    if (E <= 64) SDMOE_TOPK_MASK(1, 0);
+    else if (E <= 128) SDMOE_TOPK_MASK(2, 0);
+    else SDMOE_TOPK_MASK(4, 0);
+  }
+#undef SDMOE_TOPK_MASK
   SDMOE_CHECK_LAUNCH();
   return SDMOE_OK;
 }

@@ -32,11 +32,15 @@ def main():
     ap.add_argument("--stages", type=int, default=0)
     ap.add_argument("--tile", type=int, default=0, help="forced GEMM tile (sdmoe_tune knob 1), 0 = auto")
     ap.add_argument("--only", default="", help="run only rows whose label contains this")
+    ap.add_argument("--bk", type=int, default=0, help="GEMM K-step depth (sdmoe_tune knob 2), 0 = auto")
+    ap.add_argument("--prio", type=int, default=0, help="s_setprio around the MFMA block (knob 3)")
     a = ap.parse_args()
     from sdmoe import _lib
     _lib.check(_lib.load().sdmoe_tune(0, a.stages), "tune")
     _lib.check(_lib.load().sdmoe_tune(1, a.tile), "tune")
-    print("stages", a.stages, "tile", a.tile)
+    _lib.check(_lib.load().sdmoe_tune(2, a.bk), "tune")
+    _lib.check(_lib.load().sdmoe_tune(3, a.prio), "tune")
+    print("stages", a.stages, "tile", a.tile, "bk", a.bk)
     n = a.nimg
     dev = "cuda"
     rows = []
@@ -60,6 +64,26 @@ def main():
         w = (torch.randn(N, K, device=dev) * K ** -0.5).half()
         ms = timeit(lambda: ops.linear(x, w), a.iters)
         rows.append((f"linear M={M} N={N} K={K}", ms, 2.0 * M * N * K / ms / 1e9))
+    # fused routed GEGLU: projection GEMM with value*act(gate) + expert-score epilogue, then the top-k mask
+    for M, C in [(n * 4096, 320), (n * 1024, 640), (n * 256, 1280)]:
+        F, E = 4 * C, C // 5
+        x = torch.randn(M, C, device=dev).half()
+        w = (torch.randn(2 * F, C, device=dev) * C ** -0.5).half()
+        b = torch.zeros(2 * F, device=dev).half()
+        routing = ops.Routing(torch.arange(F) % E, E, E // 5, dev)
+        w_il, b_il = ops.interleave_geglu(w, b, routing.perm)
+        score = torch.empty(M, E, device=dev).half()
+        out = torch.empty(M, F, device=dev).half()
+        ms = timeit(lambda: ops.linear_geglu(x, w_il, b_il, ops.ACT_RELU, score=score, esize=routing.esize, out=out),
+                    a.iters)
+        rows.append((f"geglu-gemm M={M} F={F} K={C}", ms, 2.0 * M * 2 * F * C / ms / 1e9))
+        ms = timeit(lambda: ops.moe_topk_mask(out, score, routing), a.iters)
+        rows.append((f"topk-mask M={M} F={F} (GB/s)", ms, (M * F * 2 * 0.8 + M * E * 2) / ms / 1e6))
+        y = torch.empty(M, 2 * F, device=dev).half()
+        ms = timeit(lambda: ops.linear(x, w, b, out=y), a.iters)
+        rows.append((f"  unfused proj M={M} N={2 * F} K={C}", ms, 2.0 * M * 2 * F * C / ms / 1e9))
+        ms = timeit(lambda: ops.geglu_route(y, routing, ops.ACT_RELU, out=out), a.iters)
+        rows.append((f"  unfused route M={M} F={F} (GB/s)", ms, (M * F * 6) / ms / 1e6))
     for N_, d, Nk in [(4096, 40, 4096), (4096, 40, 77), (1024, 80, 1024), (256, 160, 256)]:
         C = 8 * d
         q = torch.randn(n * N_, 3 * C, device=dev).half()
