@@ -98,48 +98,46 @@ __global__ __launch_bounds__(64) void gn_finalize_kernel(const half_t* __restric
   }
 }
 
-// LayerNorm over the last dim (C <= 2048, C % 8 == 0), one wave per row, values kept in registers.
-template <int MAXCH>
+// LayerNorm over the last dim (C % 64 == 0, C <= 2048): 8 lanes per row, 8 rows per wave, 32 rows per block;
+// lane (row r = lane/8, sub = lane%8) holds 16-B chunks sub, sub+8, ... (128-B coalesced per 8 lanes), two-pass
+// mean / variance in registers with 8-lane xor reductions.
+template <int CPL>  // chunks per lane = C / 64
 __global__ __launch_bounds__(256) void layernorm_kernel(const half_t* __restrict__ X, long ldx, half_t* __restrict__ Y,
                                                         long ldy, int M, int C, const half_t* __restrict__ gamma,
                                                         const half_t* __restrict__ beta, float eps) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= M) return;
-  const int nch = C / 8;
-  half8 v[MAXCH];
+  const int lane = threadIdx.x & 63, sub = lane & 7;
+  const int row = blockIdx.x * 32 + (threadIdx.x >> 6) * 8 + (lane >> 3);
+  const bool live = row < M;
+  const half_t* xr = X + (long)(live ? row : 0) * ldx;
+  half8 v[CPL];
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) v[i] = *reinterpret_cast<const half8*>(xr + (sub + 8 * i) * 8);
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < MAXCH; ++i) {
-    const int c = lane + 64 * i;
-    if (c < nch) {
-      v[i] = *reinterpret_cast<const half8*>(X + (long)row * ldx + c * 8);
+  for (int i = 0; i < CPL; ++i)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s += (float)v[i][j];
-    }
-  }
-  const float mean = wave_sum(s) / C;
+    for (int j = 0; j < 8; ++j) s += (float)v[i][j];
+#pragma unroll
+  for (int o = 1; o < 8; o <<= 1) s += __shfl_xor(s, o, 64);
+  const float mean = s / C;
   float q = 0.f;
 #pragma unroll
-  for (int i = 0; i < MAXCH; ++i) {
-    const int c = lane + 64 * i;
-    if (c < nch) {
+  for (int i = 0; i < CPL; ++i)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { const float d = (float)v[i][j] - mean; q += d * d; }
-    }
-  }
-  const float rstd = rsqrtf(wave_sum(q) / C + eps);
+    for (int j = 0; j < 8; ++j) { const float d = (float)v[i][j] - mean; q = __builtin_fmaf(d, d, q); }
 #pragma unroll
-  for (int i = 0; i < MAXCH; ++i) {
-    const int c = lane + 64 * i;
-    if (c < nch) {
-      half8 gm = *reinterpret_cast<const half8*>(gamma + c * 8);
-      half8 bt = *reinterpret_cast<const half8*>(beta + c * 8);
-      half8 o;
+  for (int o = 1; o < 8; o <<= 1) q += __shfl_xor(q, o, 64);
+  const float rstd = rsqrtf(q / C + eps);
+  if (!live) return;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = (half_t)(((float)v[i][j] - mean) * rstd * (float)gm[j] + (float)bt[j]);
-      *reinterpret_cast<half8*>(Y + (long)row * ldy + c * 8) = o;
-    }
+  for (int i = 0; i < CPL; ++i) {
+    const int c = (sub + 8 * i) * 8;
+    const half8 gm = *reinterpret_cast<const half8*>(gamma + c);
+    const half8 bt = *reinterpret_cast<const half8*>(beta + c);
+    half8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (half_t)(((float)v[i][j] - mean) * rstd * (float)gm[j] + (float)bt[j]);
+    *reinterpret_cast<half8*>(Y + (long)row * ldy + c) = o;
   }
 }
 
@@ -174,18 +172,21 @@ extern "C" int sdmoe_layernorm(const void* X, long ldx, void* Y, long ldy, int M
                                const void* beta, float eps, void* stream) {
   if (!X || !Y || !gamma || !beta || M < 0 || C <= 0) return SDMOE_EARG;
   if (M == 0) return SDMOE_OK;
-  if (C % 8 || ldx % 8 || ldy % 8 || C > 2048) return SDMOE_ESHAPE;
+  if (C % 64 || ldx % 8 || ldy % 8 || C > 2048) return SDMOE_ESHAPE;
   hipStream_t s = (hipStream_t)stream;
-  const int blocks = (M + 3) / 4;
-  if (C <= 512)
-    layernorm_kernel<1><<<blocks, 256, 0, s>>>((const half_t*)X, ldx, (half_t*)Y, ldy, M, C, (const half_t*)gamma,
-                                               (const half_t*)beta, eps);
-  else if (C <= 1024)
-    layernorm_kernel<2><<<blocks, 256, 0, s>>>((const half_t*)X, ldx, (half_t*)Y, ldy, M, C, (const half_t*)gamma,
-                                               (const half_t*)beta, eps);
-  else
-    layernorm_kernel<4><<<blocks, 256, 0, s>>>((const half_t*)X, ldx, (half_t*)Y, ldy, M, C, (const half_t*)gamma,
-                                               (const half_t*)beta, eps);
+  const int blocks = (M + 31) / 32;
+  const half_t* x = (const half_t*)X;
+  half_t* y = (half_t*)Y;
+  const half_t* g = (const half_t*)gamma;
+  const half_t* b = (const half_t*)beta;
+  switch (C / 64) {
+#define SDMOE_LN(n) \
+    case n: layernorm_kernel<n><<<blocks, 256, 0, s>>>(x, ldx, y, ldy, M, C, g, b, eps); break;
+    SDMOE_LN(1) SDMOE_LN(2) SDMOE_LN(3) SDMOE_LN(4) SDMOE_LN(5) SDMOE_LN(6) SDMOE_LN(8) SDMOE_LN(10)
+    SDMOE_LN(12) SDMOE_LN(16) SDMOE_LN(20) SDMOE_LN(24) SDMOE_LN(32)
+#undef SDMOE_LN
+    default: return SDMOE_EUNSUP;
+  }
   SDMOE_CHECK_LAUNCH();
   return SDMOE_OK;
 }

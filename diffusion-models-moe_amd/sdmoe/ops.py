@@ -59,6 +59,17 @@ def _workspace(device):
     return ws
 
 
+_GN_WS = {}
+
+
+def _gn_workspace(device, floats):
+    """GroupNorm partial-sum scratch (reused across calls; no allocation per call)."""
+    ws = _GN_WS.get(device)
+    if ws is None or ws.numel() < floats:
+        ws = _GN_WS[device] = torch.zeros(max(floats, 1 << 16), dtype=torch.float32, device=device)
+    return ws
+
+
 def groupnorm_apply(x, nimg, HW, scale, shift, silu, out=None):
     """out = (SiLU?)(x * scale[img, c] + shift[img, c]) on [nimg*HW, C] views."""
     lib = _lib.load()
@@ -157,7 +168,7 @@ def groupnorm_stats(x, nimg, HW, gamma, beta, eps, groups=32):
     C = x.shape[1]
     scale = torch.empty((nimg, C), dtype=torch.float32, device=x.device)
     shift = torch.empty((nimg, C), dtype=torch.float32, device=x.device)
-    ws = torch.empty((nimg * groups * 64 * 2,), dtype=torch.float32, device=x.device)
+    ws = _gn_workspace(x.device, nimg * groups * 64 * 2)
     st = lib.sdmoe_groupnorm_stats(xp, ldx, nimg, HW, C, groups, _dev(gamma, "gamma"), _dev(beta, "beta"),
                                    float(eps), scale.data_ptr(), shift.data_ptr(), ws.data_ptr(), ws.numel(),
                                    _stream())

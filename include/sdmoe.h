@@ -72,7 +72,7 @@ int sdmoe_groupnorm_stats(const void* X, long ldx, int nimg, int HW, int C, int 
                           const void* beta, float eps, float* scale, float* shift, float* workspace,
                           long workspace_floats, void* stream);
 
-/* LayerNorm over the last dimension (C % 8 == 0, C <= 2048). Replaces BasicTransformerBlock norm1/2/3. */
+/* LayerNorm over the last dimension (C % 64 == 0, C <= 2048). Replaces BasicTransformerBlock norm1/2/3. */
 int sdmoe_layernorm(const void* X, long ldx, void* Y, long ldy, int M, int C, const void* gamma, const void* beta,
                     float eps, void* stream);
 
