@@ -31,12 +31,14 @@ def main():
     ap.add_argument("fetch_csv")
     ap.add_argument("write_csv")
     ap.add_argument("--kernel", default="gemm_kernel<")
-    ap.add_argument("--mode", default="1", help="3rd template arg of gemm_kernel (1 = conv); '' = any")
+    ap.add_argument("--mode", default="1,2", help="comma list of gemm_kernel MODE values (5th template arg: "
+                    "1 = conv, 2 = conv with fused upsample); '' = any")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     fetch, names = load(a.fetch_csv, "FETCH_SIZE")
     write, wnames = load(a.write_csv, "WRITE_SIZE")
-    pat = re.compile(r"gemm_kernel<\d+, \d+, (\d+), \d+>")
+    pat = re.compile(r"gemm_kernel<\d+, \d+, \d+, \d+, (\d+), \d+, \d+>")
+    modes = set(a.mode.split(",")) if a.mode else set()
 
     def keep(n):
         if a.kernel not in n:
@@ -44,7 +46,7 @@ def main():
         if a.mode == "":
             return True
         m = pat.search(n)
-        return bool(m) and m.group(1) == a.mode
+        return bool(m) and m.group(1) in modes
     f_sel = [v for d, v in fetch.items() if keep(names[d])]
     w_sel = [v for d, v in write.items() if keep(wnames[d])]
     if not f_sel or not w_sel:
