@@ -27,7 +27,8 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-TFLOP_PER_IMAGE = 81.34       # SD-1.x 512^2, 50 steps, CFG, MoE scoring on
+TFLOP_PER_IMAGE = {"sd14": 81.34,   # SD-1.x 512^2, 50 steps, CFG, MoE scoring on
+                   "sdxl": 694.9}   # SDXL-base 1024^2, 50 steps, CFG, MoE scoring on
 PEAK_FP16_TFLOPS = 2500.0     # MI355X dense FP16/BF16 MFMA (MI355X_MICROARCH.md, chip table)
 
 
@@ -36,7 +37,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=2)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--batch", type=int, default=8, help="prompts per GPU (config 4: 64 prompts / 8 GPUs)")
+    p.add_argument("--model", choices=["sd14", "sdxl"], default="sd14",
+                   help="sd14: SD-1.4 512^2 (the metric, configs 2-4); sdxl: SDXL-base 1024^2 (config 5)")
+    p.add_argument("--batch", type=int, default=None,
+                   help="prompts per GPU (default 8 = config 4's 64 prompts / 8 GPUs; 2 for sdxl)")
     p.add_argument("--inference-steps", type=int, default=50)
     p.add_argument("--mask", choices=["remove", "union", "none"], default="remove")
     p.add_argument("--topk", type=float, default=0.2)
@@ -79,7 +83,7 @@ def build(args, world, rank, dev):
     from neuron_receivers import RemoveExperts, MOEFy, WandaRemoveNeuronsFast
     from sdmoe import distributed as D
 
-    cfg = UNetConfig.sd14(64)
+    cfg = UNetConfig.sdxl(128) if args.model == "sdxl" else UNetConfig.sd14(64)
     pipe = StableDiffusionPipeline.synthetic(cfg, seed=0, device=dev, num_inference_steps=args.inference_steps)
     find_and_change_geglu(pipe.unet)                  # relufied U-Net (config 2/3)
     moefy_synthetic(pipe, args.topk, 20, seed=0)      # E = 4C/20 experts, k = int(E*topk)
@@ -210,6 +214,8 @@ def cpu_baseline(args):
 
 def main():
     args = parse()
+    if args.batch is None:
+        args.batch = 2 if args.model == "sdxl" else 8
     world, rank, local = setup_dist(args.gpus)
     dev = f"cuda:{local}" if world > 1 else "cuda:0"
     from sdmoe import ops, _lib
@@ -278,7 +284,7 @@ def main():
                     "launches": n, "avg_launch_ms": round(ms / n, 4),
                     "algorithmic_flop_per_launch": round(flops / n)}
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.model == "sd14":
         cpu = cpu_baseline(args)
     if rank == 0:
         line = {
@@ -286,13 +292,14 @@ def main():
             "value": round(value, 4), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp16", "data": "synthetic",
-            "config": {"workload": f"SD-1.4 MoE-fied (relu, top-k {args.topk}, expert 20) + "
+            "config": {"workload": f"{'SDXL-base' if args.model == 'sdxl' else 'SD-1.4'} MoE-fied (relu, top-k {args.topk}, expert 20) + "
                                    f"{'RemoveExperts skilled-expert mask' if args.mask != 'none' else 'no mask'}"
-                                   f"{' + union Wanda mask' if args.mask == 'union' else ''}, 512^2 "
-                                   f"(4x64x64 latents), {args.inference_steps} DDIM steps, CFG 7.5",
+                                   f"{' + union Wanda mask' if args.mask == 'union' else ''}, "
+                                   f"{8 * cfg.sample_size}^2 (4x{cfg.sample_size}x{cfg.sample_size} latents), "
+                                   f"{args.inference_steps} DDIM steps, CFG 7.5",
                        "prompts_per_gpu": args.batch, "global_batch": world * args.batch,
                        "parallelism": f"dp{world}"},
-            "step_mfma_frac": round(value / world * TFLOP_PER_IMAGE / PEAK_FP16_TFLOPS, 4),
+            "step_mfma_frac": round(value / world * TFLOP_PER_IMAGE[args.model] / PEAK_FP16_TFLOPS, 4),
             "roofline": roof, "cpu_baseline": cpu, "outputs_finite": finite,
         }
         print(json.dumps(line), flush=True)

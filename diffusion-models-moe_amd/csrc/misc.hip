@@ -19,6 +19,23 @@ __global__ void timestep_embedding_kernel(half_t* out, const float* tptr, float 
   }
 }
 
+// n timesteps t_dev[0..n) -> rows; row r lands at out + (r / group) * ldo + (r % group) * dim (SDXL text_time:
+// the 6 time-id sinusoids of an image sit side by side in its add-embedding input row)
+__global__ void timestep_embedding_rows_kernel(half_t* out, long ldo, const float* t_dev, int group, int dim,
+                                               int flip, float freq_shift) {
+  const int r = blockIdx.x;
+  half_t* o = out + (long)(r / group) * ldo + (long)(r % group) * dim;
+  const int half = dim / 2;
+  const float t = t_dev[r];
+  for (int i = threadIdx.x; i < half; i += blockDim.x) {
+    const float expo = -logf(10000.0f) * (float)i / ((float)half - freq_shift);
+    const float a = t * expf(expo);
+    const float sv = sinf(a), cv = cosf(a);
+    if (flip) { o[i] = (half_t)cv; o[half + i] = (half_t)sv; }
+    else { o[i] = (half_t)sv; o[half + i] = (half_t)cv; }
+  }
+}
+
 // latents fp32 NCHW [B,4,H,W] -> U-Net input fp16 NHWC [ncopy*B, H*W, ldo] (channels 0..3; CFG copies)
 __global__ void prepare_input_kernel(const float* __restrict__ lat, half_t* __restrict__ out, int B, int HW,
                                      long ldo, int ncopy) {
@@ -88,6 +105,16 @@ extern "C" int sdmoe_timestep_embedding(void* out, const float* t_dev, float t, 
   if (!out || dim <= 0 || dim % 2) return SDMOE_EARG;
   timestep_embedding_kernel<<<1, 256, 0, (hipStream_t)stream>>>((half_t*)out, t_dev, t, dim, flip_sin_to_cos,
                                                                 freq_shift);
+  SDMOE_CHECK_LAUNCH();
+  return SDMOE_OK;
+}
+
+extern "C" int sdmoe_timestep_embedding_rows(void* out, long ldo, const float* t_dev, int n, int group, int dim,
+                                             int flip_sin_to_cos, float freq_shift, void* stream) {
+  if (!out || !t_dev || n <= 0 || group <= 0 || dim <= 0 || dim % 2) return SDMOE_EARG;
+  if (ldo < (long)group * dim) return SDMOE_ESHAPE;
+  timestep_embedding_rows_kernel<<<n, 128, 0, (hipStream_t)stream>>>((half_t*)out, ldo, t_dev, group, dim,
+                                                                     flip_sin_to_cos, freq_shift);
   SDMOE_CHECK_LAUNCH();
   return SDMOE_OK;
 }

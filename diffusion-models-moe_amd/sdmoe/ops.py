@@ -331,6 +331,20 @@ def timestep_embedding(t: float, dim: int, device, flip_sin_to_cos=True, freq_sh
     return out
 
 
+def timestep_embedding_rows(t_dev: torch.Tensor, dim: int, out: torch.Tensor, group: int = 1,
+                            flip_sin_to_cos=True, freq_shift=0.0):
+    """Sinusoids of t_dev (fp32 [n]) into `out` (2-D fp16 view): row r at out[r // group, (r % group)*dim:]."""
+    lib = _lib.load()
+    op, ldo = _rows(out, "out")
+    n = t_dev.numel()
+    if out.shape[0] * group < n or out.shape[1] < group * dim:
+        raise ValueError("timestep_embedding_rows: output view too small")
+    st = lib.sdmoe_timestep_embedding_rows(op, ldo, _dev(t_dev, "t_dev", torch.float32), n, group, dim,
+                                           int(bool(flip_sin_to_cos)), float(freq_shift), _stream())
+    _lib.check(st, "sdmoe_timestep_embedding_rows")
+    return out
+
+
 def prepare_input(lat: torch.Tensor, out: torch.Tensor, ncopy: int):
     lib = _lib.load()
     B, C, H, W = lat.shape

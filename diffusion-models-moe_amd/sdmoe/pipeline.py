@@ -40,6 +40,17 @@ def prompt_embedding(prompt: str, dim: int = 768) -> torch.Tensor:
     return torch.from_numpy((rng.standard_normal((CTX_LEN, dim)) * 0.5).astype(np.float32))
 
 
+def pooled_embedding(prompt: str, dim: int = 1280) -> torch.Tensor:
+    """Seeded synthetic pooled text embedding [dim] (SDXL text_embeds; CLIP-G pooled output stand-in)."""
+    rng = np.random.default_rng(zlib.crc32(("pooled:" + prompt).encode("utf-8")))
+    return torch.from_numpy((rng.standard_normal(dim) * 0.5).astype(np.float32))
+
+
+def sdxl_time_ids(height: int, width: int) -> list:
+    """SDXL micro-conditioning (original_size, crops_coords_top_left, target_size) for an uncropped image."""
+    return [float(height), float(width), 0.0, 0.0, float(height), float(width)]
+
+
 def initial_latents(seed: int, index: int, cfg: UNetConfig) -> torch.Tensor:
     """Per-prompt latents from a CPU generator seeded by (seed, global prompt index): identical for any
     world size / sharding."""
@@ -67,11 +78,27 @@ class StableDiffusionPipeline:
         unet = UNet2DConditionModel.from_state_dict(make_state_dict(cfg, seed), cfg, device)
         return cls(unet, device, **kw)
 
+    @property
+    def is_sdxl(self):
+        return self.config.addition_embed_type == "text_time"
+
     def encode_prompt(self, prompts):
-        """[uncond x B ; cond x B] context rows [2B*77, dim] fp16 on device (uncond first, as diffusers)."""
+        """[uncond x B ; cond x B] context rows [2B*77, dim] fp16 on device (uncond first, as diffusers).
+        SDXL base sets force_zeros_for_empty_prompt: the unconditional embeddings are zeros."""
         dim = self.config.cross_attention_dim
-        embs = [prompt_embedding("", dim)] * len(prompts) + [prompt_embedding(p, dim) for p in prompts]
+        unc = torch.zeros(CTX_LEN, dim) if self.is_sdxl else prompt_embedding("", dim)
+        embs = [unc] * len(prompts) + [prompt_embedding(p, dim) for p in prompts]
         return torch.cat(embs, 0).to(self.device, torch.float16).contiguous()
+
+    def added_cond(self, prompts):
+        """SDXL added_cond_kwargs rows [uncond x B ; cond x B]: pooled text_embeds [2B, pooled] and time_ids
+        [2B, 6] (1024^2 uncropped at sample_size 128)."""
+        cfg = self.config
+        d = cfg.pooled_dim
+        pooled = torch.stack([torch.zeros(d)] * len(prompts) + [pooled_embedding(p, d) for p in prompts])
+        px = 8 * cfg.sample_size
+        tids = torch.tensor([sdxl_time_ids(px, px)] * (2 * len(prompts)), dtype=torch.float32)
+        return {"text_embeds": pooled, "time_ids": tids}
 
     def __call__(self, prompt, num_inference_steps=None, guidance_scale=None, latents=None, seed=None,
                  prompt_offset=None, safety_checker=None, output_type="latent", **unused):
@@ -90,6 +117,12 @@ class StableDiffusionPipeline:
         lat = latents.to(self.device, torch.float32).contiguous()
         ncopy = 2 if do_cfg else 1
         ctx = self.encode_prompt(prompts)
+        add_hidden = None
+        if self.is_sdxl:
+            ac = self.added_cond(prompts)
+            add_hidden = self.unet.add_embed_hidden(ac["text_embeds"], ac["time_ids"])  # once per call
+            if not do_cfg:
+                add_hidden = add_hidden[B:]
         if not do_cfg:
             ctx = ctx[B * CTX_LEN:]
         HW = cfg.sample_size * cfg.sample_size
@@ -98,7 +131,7 @@ class StableDiffusionPipeline:
         ops.prepare_input(lat, x_in, ncopy)
         ts, a_t, a_prev = ddim_schedule(steps)
         for s, t in enumerate(ts):
-            self.unet.forward_nhwc(x_in, float(t), ctx, out=eps)
+            self.unet.forward_nhwc(x_in, float(t), ctx, out=eps, add_hidden=add_hidden)
             ops.cfg_ddim_step(eps, lat, do_cfg, g, a_t[s], a_prev[s], next_in=x_in)
         return PipelineOutput(images=[lat[i] for i in range(B)])
 

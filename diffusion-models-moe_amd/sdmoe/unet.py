@@ -264,17 +264,21 @@ class BasicTransformerBlock(nn.Module):
 
 
 class Transformer2DModel(nn.Module):
-    def __init__(self, norm, proj_in, block, proj_out):
+    """GroupNorm -> proj_in -> transformer_blocks (1 for SD-1.x, up to 10 for SDXL) -> proj_out (+ input).
+    proj_in/out are 1x1 convs (SD-1.x) or Linears (SDXL use_linear_projection): the same [C, C] GEMM on NHWC."""
+
+    def __init__(self, norm, proj_in, blocks, proj_out):
         super().__init__()
         self.norm = norm
         self.proj_in = proj_in
-        self.transformer_blocks = nn.ModuleList([block])
+        self.transformer_blocks = nn.ModuleList(blocks)
         self.proj_out = proj_out
 
     def run(self, x, nimg, HW, ctx2d, out):
         sc, sh = self.norm.stats(x, nimg, HW)
         hs = self.proj_in.run(x, gn=(sc, sh, False), rows_per_batch=HW)
-        hs = self.transformer_blocks[0].run(hs, nimg, HW, ctx2d)
+        for blk in self.transformer_blocks:
+            hs = blk.run(hs, nimg, HW, ctx2d)
         return self.proj_out.run(hs, residual=x, out=out)
 
 
@@ -289,8 +293,11 @@ class ResnetBlock2D(nn.Module):
         HW = H * W
         sc1, sh1 = self.norm1.stats(x, nimg, HW)
         o, n = self.temb_slice
+        # temb_all: [1, sum Cout] (SD-1.x, one timestep embedding for the batch) or [nimg, sum Cout] (SDXL:
+        # per-image text_time conditioning) -> per-image column add in the conv epilogue
+        bstride = temb_all.stride(0) if temb_all.shape[0] > 1 else 0
         h = ops.conv3x3(x, nimg, H, W, self.conv1.weight, self.conv1.bias, gn=(sc1, sh1, True),
-                        coladd=temb_all[:, o:o + n], coladd_bstride=0)
+                        coladd=temb_all[:, o:o + n], coladd_bstride=bstride)
         sc2, sh2 = self.norm2.stats(h, nimg, HW)
         res = x if self.conv_shortcut is None else self.conv_shortcut.run(x)
         return ops.conv3x3(h, nimg, H, W, self.conv2.weight, self.conv2.bias, gn=(sc2, sh2, True), residual=res,
@@ -363,21 +370,33 @@ class UNet2DConditionModel(nn.Module):
             return ResnetBlock2D(gn(p + ".norm1", cfg.norm_eps), conv(p + ".conv1"), lin(p + ".time_emb_proj"),
                                  gn(p + ".norm2", cfg.norm_eps), conv(p + ".conv2"), sc)
 
-        def transformer(p):
-            b = p + ".transformer_blocks.0"
+        def block(b):
+            heads = cfg.heads_for(sd[b + ".attn1.to_q.weight"].shape[0])
             a1 = Attention(t(b + ".attn1.to_q.weight"), t(b + ".attn1.to_k.weight"), t(b + ".attn1.to_v.weight"),
-                           t(b + ".attn1.to_out.0.weight"), t(b + ".attn1.to_out.0.bias"), cfg.attention_heads, True)
+                           t(b + ".attn1.to_out.0.weight"), t(b + ".attn1.to_out.0.bias"), heads, True)
             a2 = Attention(t(b + ".attn2.to_q.weight"), t(b + ".attn2.to_k.weight"), t(b + ".attn2.to_v.weight"),
-                           t(b + ".attn2.to_out.0.weight"), t(b + ".attn2.to_out.0.bias"), cfg.attention_heads, False)
+                           t(b + ".attn2.to_out.0.weight"), t(b + ".attn2.to_out.0.bias"), heads, False)
             ff = FeedForward(GEGLU(lin(b + ".ff.net.0.proj")), lin(b + ".ff.net.2"))
-            blk = BasicTransformerBlock(ln(b + ".norm1"), a1, ln(b + ".norm2"), a2, ln(b + ".norm3"), ff)
-            return Transformer2DModel(gn(p + ".norm", cfg.transformer_norm_eps), conv1x1(p + ".proj_in"), blk,
+            return BasicTransformerBlock(ln(b + ".norm1"), a1, ln(b + ".norm2"), a2, ln(b + ".norm3"), ff)
+
+        def transformer(p):
+            blocks = []
+            while f"{p}.transformer_blocks.{len(blocks)}.norm1.weight" in sd:
+                blocks.append(block(f"{p}.transformer_blocks.{len(blocks)}"))
+            return Transformer2DModel(gn(p + ".norm", cfg.transformer_norm_eps), conv1x1(p + ".proj_in"), blocks,
                                       conv1x1(p + ".proj_out"))
 
         w_in = sd["conv_in.weight"].to(dev, torch.float16)
         w_in = F.pad(w_in, (0, 0, 0, 0, 0, IN_PAD - w_in.shape[1])).permute(0, 2, 3, 1).contiguous()
         m.conv_in = Conv2d(w_in, t("conv_in.bias"))
         m.time_embedding = TimestepEmbedding(lin("time_embedding.linear_1"), lin("time_embedding.linear_2"))
+        if cfg.addition_embed_type == "text_time":
+            a1 = lin("add_embedding.linear_1")
+            k_real = a1.weight.shape[1]
+            kp = (k_real + 63) // 64 * 64  # K padded to the GEMM's 64-wide K-step (zero columns)
+            a1.weight = _buf(F.pad(a1.weight.data, (0, kp - k_real)).contiguous())
+            m.add_embedding = TimestepEmbedding(a1, lin("add_embedding.linear_2"))
+            m.add_in_features = k_real
         nblk = len(cfg.block_out_channels)
         L = cfg.layers_per_block
         downs = []
@@ -419,17 +438,42 @@ class UNet2DConditionModel(nn.Module):
         return m
 
     # ------------------------------------------------------------------ forward
-    def time_embed(self, t, t_dev=None):
+    def add_embed_hidden(self, text_embeds, time_ids):
+        """SDXL text_time conditioning, step-invariant half: SiLU(add_embedding.linear_1([text_embeds ;
+        sinusoid(time_ids)])) [nimg, temb] fp16 (UNet2DConditionModel.get_aug_embed). Computed once per
+        pipeline call; the per-step half is in time_embed()."""
+        cfg = self.config
+        dev = self.conv_in.weight.device
+        n = time_ids.shape[0]
+        d = cfg.addition_time_embed_dim
+        kp = self.add_embedding.linear_1.weight.shape[1]
+        add = torch.zeros((n, kp), dtype=torch.float16, device=dev)
+        add[:, :text_embeds.shape[1]] = text_embeds.to(dev, torch.float16)
+        tid = time_ids.to(dev, torch.float32).reshape(-1).contiguous()
+        p = text_embeds.shape[1]
+        ops.timestep_embedding_rows(tid, d, add[:, p:p + 6 * d], group=6, flip_sin_to_cos=cfg.flip_sin_to_cos,
+                                    freq_shift=cfg.freq_shift)
+        return self.add_embedding.linear_1.run(add, act=ops.ACT_SILU)
+
+    def time_embed(self, t, t_dev=None, add_hidden=None):
         cfg = self.config
         dev = self.conv_in.weight.device
         e = ops.timestep_embedding(t, cfg.block_out_channels[0], dev, cfg.flip_sin_to_cos, cfg.freq_shift, t_dev=t_dev)
         e = self.time_embedding.linear_1.run(e, act=ops.ACT_SILU)
-        e = self.time_embedding.linear_2.run(e, act=ops.ACT_SILU)  # every consumer applies SiLU(temb) first
+        if cfg.addition_embed_type == "text_time":
+            # emb = linear_2(...) + add_embedding(...); every consumer applies SiLU(emb) first:
+            # SiLU(add_hidden @ W2a^T + b2a + e_t) with e_t broadcast to every image by the column-add epilogue
+            e = self.time_embedding.linear_2.run(e)
+            e = self.add_embedding.linear_2.run(add_hidden, act=ops.ACT_SILU, coladd=e, coladd_bstride=0,
+                                                rows_per_batch=add_hidden.shape[0])
+        else:
+            e = self.time_embedding.linear_2.run(e, act=ops.ACT_SILU)  # every consumer applies SiLU(temb) first
         return ops.linear(e, self.temb_w, self.temb_b)
 
-    def forward_nhwc(self, x_in, t, ctx2d, out=None, t_dev=None):
-        """One U-Net evaluation. x_in: [nimg*H*W, 64] fp16 (channels 0..3 = latent), ctx2d: [nimg*77, 768].
-        Returns eps as [nimg*H*W, 8] fp16 (channels 0..3 valid)."""
+    def forward_nhwc(self, x_in, t, ctx2d, out=None, t_dev=None, add_hidden=None):
+        """One U-Net evaluation. x_in: [nimg*H*W, 64] fp16 (channels 0..3 = latent), ctx2d: [nimg*77, ctx dim].
+        add_hidden (SDXL): add_embed_hidden(text_embeds, time_ids). Returns eps as [nimg*H*W, 8] fp16
+        (channels 0..3 valid)."""
         cfg = self.config
         dev = x_in.device
         nimg = ctx2d.shape[0] // CTX_LEN
@@ -437,7 +481,7 @@ class UNet2DConditionModel(nn.Module):
         ch = cfg.block_out_channels
         nblk = len(ch)
         L = cfg.layers_per_block
-        temb_all = self.time_embed(t, t_dev)
+        temb_all = self.time_embed(t, t_dev, add_hidden)
 
         # ---- plan the up-path concat buffers [rows, C_prev + C_skip] (consumption order)
         rev = list(reversed(ch))
@@ -526,11 +570,15 @@ class UNet2DConditionModel(nn.Module):
             out = new(nimg * H * W, OUT_PAD)
         return ops.conv3x3(final, nimg, H, W, self.conv_out.weight, self.conv_out.bias, gn=(sc, sh, True), out=out)
 
-    def forward(self, sample, timestep, encoder_hidden_states):
-        """diffusers-style call: sample [n, 4, H, W], encoder_hidden_states [n, 77, ctx]; returns eps [n,4,H,W]."""
+    def forward(self, sample, timestep, encoder_hidden_states, added_cond_kwargs=None):
+        """diffusers-style call: sample [n, 4, H, W], encoder_hidden_states [n, 77, ctx]; returns eps [n,4,H,W].
+        added_cond_kwargs (SDXL): {"text_embeds": [n, pooled], "time_ids": [n, 6]}, as diffusers."""
         n, c, H, W = sample.shape
         x = torch.zeros((n * H * W, IN_PAD), dtype=torch.float16, device=sample.device)
         x[:, :c] = sample.permute(0, 2, 3, 1).reshape(n * H * W, c).to(torch.float16)
         ctx = encoder_hidden_states.reshape(-1, encoder_hidden_states.shape[-1]).to(torch.float16).contiguous()
-        eps = self.forward_nhwc(x, float(timestep), ctx)
+        add_hidden = None
+        if self.config.addition_embed_type == "text_time":
+            add_hidden = self.add_embed_hidden(added_cond_kwargs["text_embeds"], added_cond_kwargs["time_ids"])
+        eps = self.forward_nhwc(x, float(timestep), ctx, add_hidden=add_hidden)
         return eps[:, :c].reshape(n, H, W, c).permute(0, 3, 1, 2).contiguous()

@@ -27,11 +27,9 @@ def _resnet(prefix, cin, cout, temb):
     return p
 
 
-def _transformer(prefix, C, ctx):
-    b = f"{prefix}.transformer_blocks.0"
+def _block(b, C, ctx):
+    """BasicTransformerBlock `b` (self-attn, cross-attn, GEGLU FFN)."""
     return [
-        (f"{prefix}.norm.weight", (C,), "gn_w"), (f"{prefix}.norm.bias", (C,), "gn_b"),
-        (f"{prefix}.proj_in.weight", (C, C, 1, 1), "conv"), (f"{prefix}.proj_in.bias", (C,), "bias"),
         (f"{b}.norm1.weight", (C,), "gn_w"), (f"{b}.norm1.bias", (C,), "gn_b"),
         (f"{b}.attn1.to_q.weight", (C, C), "linear"), (f"{b}.attn1.to_k.weight", (C, C), "linear"),
         (f"{b}.attn1.to_v.weight", (C, C), "linear"),
@@ -43,8 +41,19 @@ def _transformer(prefix, C, ctx):
         (f"{b}.norm3.weight", (C,), "gn_w"), (f"{b}.norm3.bias", (C,), "gn_b"),
         (f"{b}.ff.net.0.proj.weight", (8 * C, C), "linear"), (f"{b}.ff.net.0.proj.bias", (8 * C,), "bias"),
         (f"{b}.ff.net.2.weight", (C, 4 * C), "linear_res"), (f"{b}.ff.net.2.bias", (C,), "bias"),
-        (f"{prefix}.proj_out.weight", (C, C, 1, 1), "conv_res"), (f"{prefix}.proj_out.bias", (C,), "bias"),
     ]
+
+
+def _transformer(prefix, C, ctx, depth=1, linear_proj=False):
+    """Transformer2DModel: GroupNorm, proj_in (1x1 conv, or Linear for use_linear_projection), `depth`
+    BasicTransformerBlocks, proj_out."""
+    pshape = (C, C) if linear_proj else (C, C, 1, 1)
+    p = [(f"{prefix}.norm.weight", (C,), "gn_w"), (f"{prefix}.norm.bias", (C,), "gn_b"),
+         (f"{prefix}.proj_in.weight", pshape, "conv"), (f"{prefix}.proj_in.bias", (C,), "bias")]
+    for d in range(depth):
+        p += _block(f"{prefix}.transformer_blocks.{d}", C, ctx)
+    p += [(f"{prefix}.proj_out.weight", pshape, "conv_res"), (f"{prefix}.proj_out.bias", (C,), "bias")]
+    return p
 
 
 def param_specs(cfg: UNetConfig):
@@ -58,19 +67,25 @@ def param_specs(cfg: UNetConfig):
              ("time_embedding.linear_1.bias", (temb,), "bias"),
              ("time_embedding.linear_2.weight", (temb, temb), "linear"),
              ("time_embedding.linear_2.bias", (temb,), "bias")]
+    if cfg.addition_embed_type == "text_time":
+        specs += [("add_embedding.linear_1.weight", (temb, cfg.projection_class_embeddings_input_dim), "linear"),
+                  ("add_embedding.linear_1.bias", (temb,), "bias"),
+                  ("add_embedding.linear_2.weight", (temb, temb), "linear"),
+                  ("add_embedding.linear_2.bias", (temb,), "bias")]
+    lp = cfg.use_linear_projection
     cout = ch[0]
     for i, t in enumerate(cfg.down_block_types):
         cin, cout = cout, ch[i]
         for j in range(L):
             specs += _resnet(f"down_blocks.{i}.resnets.{j}", cin if j == 0 else cout, cout, temb)
             if t.startswith("CrossAttn"):
-                specs += _transformer(f"down_blocks.{i}.attentions.{j}", cout, ctx)
+                specs += _transformer(f"down_blocks.{i}.attentions.{j}", cout, ctx, cfg.depth_of("down", i), lp)
         if i < len(ch) - 1:
             specs += [(f"down_blocks.{i}.downsamplers.0.conv.weight", (cout, cout, 3, 3), "conv"),
                       (f"down_blocks.{i}.downsamplers.0.conv.bias", (cout,), "bias")]
     C = ch[-1]
     specs += _resnet("mid_block.resnets.0", C, C, temb)
-    specs += _transformer("mid_block.attentions.0", C, ctx)
+    specs += _transformer("mid_block.attentions.0", C, ctx, cfg.depth_of("mid", 0), lp)
     specs += _resnet("mid_block.resnets.1", C, C, temb)
     rev = list(reversed(ch))
     prev = rev[0]
@@ -82,7 +97,7 @@ def param_specs(cfg: UNetConfig):
             res_in = prev if j == 0 else cout
             specs += _resnet(f"up_blocks.{i}.resnets.{j}", res_in + res_skip, cout, temb)
             if t.startswith("CrossAttn"):
-                specs += _transformer(f"up_blocks.{i}.attentions.{j}", cout, ctx)
+                specs += _transformer(f"up_blocks.{i}.attentions.{j}", cout, ctx, cfg.depth_of("up", i), lp)
         if i < len(ch) - 1:
             specs += [(f"up_blocks.{i}.upsamplers.0.conv.weight", (cout, cout, 3, 3), "conv"),
                       (f"up_blocks.{i}.upsamplers.0.conv.bias", (cout,), "bias")]

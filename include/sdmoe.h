@@ -125,6 +125,11 @@ int sdmoe_moe_topk_mask(void* P, long ldp, int M, int F, int E, int esize, int k
 /* diffusers get_timestep_embedding for one timestep (t_dev if non-NULL, else t), fp16 [dim]. */
 int sdmoe_timestep_embedding(void* out, const float* t_dev, float t, int dim, int flip_sin_to_cos, float freq_shift,
                              void* stream);
+/* n timestep embeddings (t_dev[0..n)), row r written at out + (r/group)*ldo + (r%group)*dim: SDXL's add_time_proj
+ * over the 6 micro-conditioning time ids per image (diffusers UNet2DConditionModel.get_aug_embed, "text_time";
+ * the reference loads SDXL at utils.py:111-112). */
+int sdmoe_timestep_embedding_rows(void* out, long ldo, const float* t_dev, int n, int group, int dim,
+                                  int flip_sin_to_cos, float freq_shift, void* stream);
 
 /* latents fp32 NCHW [B,4,H,W] -> U-Net input fp16 NHWC [ncopy*B, HW, ldo] channels 0..3 (CFG copies). */
 int sdmoe_prepare_input(const float* lat, void* out, int B, int HW, long ldo, int ncopy, void* stream);

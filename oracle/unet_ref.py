@@ -1,9 +1,11 @@
-"""ORACLE (test infrastructure only) — fp32 CPU restatement of the diffusers SD-1.x UNet2DConditionModel
+"""ORACLE (test infrastructure only) — fp32 CPU restatement of the diffusers SD-1.x / SDXL UNet2DConditionModel
 forward, DDIM scheduler and classifier-free-guidance loop that the reference's hooks run inside
 (utils.py:64-84 builds it; base_receiver.py:73 runs it). diffusers is not vendored in the reference and is
 absent here, so this U-Net body is PARITY-UNPINNED against diffusers itself: it restates diffusers 0.27's
 published module semantics (ResnetBlock2D, Transformer2DModel/BasicTransformerBlock, Attention, GEGLU,
-Downsample2D/Upsample2D, get_timestep_embedding, DDIMScheduler) and is checked by unit identities in
+Downsample2D/Upsample2D, get_timestep_embedding, DDIMScheduler; for SDXL also use_linear_projection,
+transformer_layers_per_block and the "text_time" add_embedding of UNet2DConditionModel.get_aug_embed — the
+reference loads SDXL at utils.py:111-112) and is checked by unit identities in
 tests/test_oracle_unet.py. The hook points reproduce where the reference's receivers attach:
   ff_hook(layer, x, proj_w, proj_b)  <- forward hook on every `ff.net.0` GEGLU (base_receiver.py:49-53)
   down_hook(layer, x, w, b)          <- forward hook on every `ff.net.2` Linear (remove_wanda_neurons_fast.py:107-112)
@@ -60,7 +62,7 @@ class UNetRef:
         return sc + h
 
     def attention(self, x, ctx, p):
-        heads = self.cfg.attention_heads
+        heads = self.cfg.heads_for(x.shape[-1])
         q = self.lin(x, p + ".to_q", bias=False)
         src = x if ctx is None else ctx
         k = self.lin(src, p + ".to_k", bias=False)
@@ -92,20 +94,41 @@ class UNetRef:
         B, C, H, W = x.shape
         res = x
         h = self.gn(x, p + ".norm", self.cfg.transformer_norm_eps)
-        h = self.conv(h, p + ".proj_in", padding=0)
-        h = h.permute(0, 2, 3, 1).reshape(B, H * W, C)
-        b = p + ".transformer_blocks.0"
-        h = self.attention(self.ln(h, b + ".norm1"), None, b + ".attn1") + h
-        h = self.attention(self.ln(h, b + ".norm2"), ctx, b + ".attn2") + h
-        h = self.feedforward(self.ln(h, b + ".norm3"), b + ".ff") + h
+        if self.cfg.use_linear_projection:
+            h = self.lin(h.permute(0, 2, 3, 1).reshape(B, H * W, C), p + ".proj_in")
+        else:
+            h = self.conv(h, p + ".proj_in", padding=0)
+            h = h.permute(0, 2, 3, 1).reshape(B, H * W, C)
+        d = 0
+        while (b := f"{p}.transformer_blocks.{d}") + ".norm1.weight" in self.sd:
+            h = self.attention(self.ln(h, b + ".norm1"), None, b + ".attn1") + h
+            h = self.attention(self.ln(h, b + ".norm2"), ctx, b + ".attn2") + h
+            h = self.feedforward(self.ln(h, b + ".norm3"), b + ".ff") + h
+            d += 1
+        if self.cfg.use_linear_projection:
+            h = self.lin(h, p + ".proj_out")
+            return h.reshape(B, H, W, C).permute(0, 3, 1, 2) + res
         h = h.reshape(B, H, W, C).permute(0, 3, 1, 2)
         return self.conv(h, p + ".proj_out", padding=0) + res
 
-    def __call__(self, sample, t, ctx, ff_hook=None, down_hook=None):
+    def aug_embed(self, text_embeds, time_ids):
+        """UNet2DConditionModel.get_aug_embed, addition_embed_type "text_time": add_time_proj (Timesteps over
+        each of the 6 time ids) flattened, concatenated after the pooled text embedding, add_embedding MLP."""
+        cfg = self.cfg
+        n = time_ids.shape[0]
+        tp = torch.cat([timestep_embedding(float(v), cfg.addition_time_embed_dim, True, 0.0)
+                        for v in time_ids.reshape(-1).tolist()]).reshape(n, -1)
+        add = torch.cat([text_embeds.float(), tp], dim=-1)
+        return self.lin(F.silu(self.lin(add, "add_embedding.linear_1")), "add_embedding.linear_2")
+
+    def __call__(self, sample, t, ctx, ff_hook=None, down_hook=None, added_cond=None):
+        """added_cond (SDXL): {"text_embeds": [n, pooled], "time_ids": [n, 6]}."""
         cfg = self.cfg
         self.ff_hook, self.down_hook, self.layer = ff_hook, down_hook, 0
         temb = timestep_embedding(t, cfg.block_out_channels[0], cfg.flip_sin_to_cos, cfg.freq_shift)
         temb = self.lin(F.silu(self.lin(temb, "time_embedding.linear_1")), "time_embedding.linear_2")
+        if cfg.addition_embed_type == "text_time":
+            temb = temb + self.aug_embed(added_cond["text_embeds"], added_cond["time_ids"])
         h = self.conv(sample, "conv_in")
         skips = [h]
         L = cfg.layers_per_block
@@ -149,9 +172,10 @@ def ddim_schedule(num_inference_steps=50, num_train_timesteps=1000, beta_start=0
 
 
 def denoise(unet: UNetRef, latents, ctx_uncond, ctx_cond, num_inference_steps=50, guidance_scale=7.5,
-            ff_hook_factory=None, down_hook_factory=None, steps=None):
+            ff_hook_factory=None, down_hook_factory=None, steps=None, added_cond=None):
     """StableDiffusionPipeline.__call__'s loop with DDIM + CFG (uncond first). Hook factories take the step
-    index and return the (layer, ...) hook for that U-Net call — the reference's (t, l) counter."""
+    index and return the (layer, ...) hook for that U-Net call — the reference's (t, l) counter.
+    added_cond (SDXL): {"text_embeds": [2B, pooled], "time_ids": [2B, 6]} rows in the [uncond; cond] order."""
     ts, a_t, a_prev = ddim_schedule(num_inference_steps)
     x = latents.float().clone()
     B = x.shape[0]
@@ -161,7 +185,7 @@ def denoise(unet: UNetRef, latents, ctx_uncond, ctx_cond, num_inference_steps=50
         inp = torch.cat([x, x])
         ffh = ff_hook_factory(s) if ff_hook_factory else None
         dh = down_hook_factory(s) if down_hook_factory else None
-        eps = unet(inp, float(ts[s]), ctx, ff_hook=ffh, down_hook=dh)
+        eps = unet(inp, float(ts[s]), ctx, ff_hook=ffh, down_hook=dh, added_cond=added_cond)
         eu, ec = eps[:B], eps[B:]
         e = eu + guidance_scale * (ec - eu)
         x0 = (x - math.sqrt(1 - a_t[s]) * e) / math.sqrt(a_t[s])

@@ -215,3 +215,42 @@ def test_modify_ffn_reads_reference_label_format(tmp_path):
     modify_ffn(g, str(tmp_path / "labels"), 0.2)
     assert tuple(g.patterns.shape) == (64, 1280) and g.k == 12 and g.patterns.dtype == torch.float16
     assert torch.equal(g.patterns.float().argmax(0), torch.from_numpy(lab))
+
+
+def test_synthetic_weights_match_sdxl_architecture():
+    """SDXL-base UNet2DConditionModel (BASELINE config 5): 2,567,463,684 params, 70 GEGLU FFNs whose sorted
+    names (helper.py:77) equal the hook execution order; the module tree carries diffusers' names."""
+    import math
+    from sdmoe.config import UNetConfig
+    from sdmoe.weights import param_specs, make_state_dict
+    from sdmoe.unet import UNet2DConditionModel
+    cfg = UNetConfig.sdxl()
+    specs = param_specs(cfg)
+    assert sum(math.prod(s) for _, s, _ in specs) == 2_567_463_684
+    geglu = sorted(n[:-len(".proj.weight")] for n, _, _ in specs if n.endswith("ff.net.0.proj.weight"))
+    assert len(geglu) == 70 and geglu == [n for n, _ in cfg.geglu_layers()]
+    assert {C for _, C in cfg.geglu_layers()} == {640, 1280}
+    assert cfg.heads_for(640) == 10 and cfg.heads_for(1280) == 20
+    tiny = UNetConfig.tiny_xl(16)
+    u = UNet2DConditionModel.from_state_dict(make_state_dict(tiny, 0), tiny, "cpu")  # construction only
+    names = [n for n, _ in u.named_modules() if n.endswith("ff.net.0")]
+    assert names == [n for n, _ in tiny.geglu_layers()] and len(names) == 28
+    assert u.add_embedding.linear_1.weight.shape[1] % 64 == 0
+
+
+def test_oracle_sdxl_micro_conditioning():
+    """The oracle's text_time add_embedding reaches the output; linear proj_in/out are used."""
+    from sdmoe.config import UNetConfig
+    from sdmoe.weights import make_state_dict
+    from oracle.unet_ref import UNetRef
+    cfg = UNetConfig.tiny_xl(8)
+    sd = make_state_dict(cfg, 1)
+    assert sd["down_blocks.1.attentions.0.proj_in.weight"].dim() == 2
+    ref = UNetRef(sd, cfg)
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(1, 4, 8, 8, generator=g)
+    ctx = torch.randn(1, 77, 128, generator=g)
+    ac = {"text_embeds": torch.randn(1, 64, generator=g), "time_ids": torch.tensor([[64., 64, 0, 0, 64, 64]])}
+    e1 = ref(x, 301.0, ctx, added_cond=ac)
+    e2 = ref(x, 301.0, ctx, added_cond={"text_embeds": ac["text_embeds"] * 0, "time_ids": ac["time_ids"]})
+    assert torch.isfinite(e1).all() and (e1 - e2).abs().max() > 1e-4
