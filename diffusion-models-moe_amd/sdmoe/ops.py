@@ -298,8 +298,9 @@ def removed_bits(expert_ids, num_experts: int, device) -> torch.Tensor:
 
 
 def geglu_route(y, routing: Routing | None, act=ACT_GELU, removed=None, out=None, gate_out=None, sel_out=None,
-                score_out=None):
-    """Routed GEGLU over y = proj(x) [M, 2F]; routing None -> dense value*act(gate)."""
+                score_out=None, k=None):
+    """Routed GEGLU over y = proj(x) [M, 2F]; routing None -> dense value*act(gate). k overrides routing.k
+    (k = E: every expert kept, i.e. the dense product plus the per-token expert scores)."""
     lib = _lib.load()
     yp, ldy = _rows(y, "y")
     M = y.shape[0]
@@ -313,11 +314,57 @@ def geglu_route(y, routing: Routing | None, act=ACT_GELU, removed=None, out=None
     else:
         if routing.F != F:
             raise ValueError(f"routing has F={routing.F}, projection gives F={F}")
-        E, k = routing.E, routing.k
+        E, k = routing.E, (routing.k if k is None else int(k))
         lab, off, nid = routing.labels.data_ptr(), routing.e_off.data_ptr(), routing.e_nid.data_ptr()
     st = lib.sdmoe_geglu_route(yp, ldy, M, F, E, k, act, lab, off, nid, _ptr(removed), op, ldo, gp, ldg,
                                _ptr(sel_out), _ptr(score_out), _stream())
     _lib.check(st, "sdmoe_geglu_route")
+    return out
+
+
+def expert_mean_topk(score, k: int, rows_per_img: int = 0, row_idx=None, mean_out=None, topk_out=None):
+    """GetExperts statistic (get_experts.py:72-80): mean of the fp16 expert scores [M, E] over all tokens, or
+    over positions row_idx (int32 device tensor) of every rows_per_img-row image, then the top-k expert ids
+    (descending, ties -> lowest id) as int32 [k]."""
+    lib = _lib.load()
+    sp, lds = _rows(score, "score")
+    M, E = score.shape
+    if topk_out is None:
+        topk_out = torch.empty(int(k), dtype=torch.int32, device=score.device)
+    rp, n_idx = (None, 0) if row_idx is None else (_dev(row_idx, "row_idx", torch.int32), row_idx.numel())
+    ws = _workspace(score.device)
+    st = lib.sdmoe_expert_mean_topk(sp, lds, M, E, int(rows_per_img), rp, n_idx, int(k),
+                                    None if mean_out is None else _dev(mean_out, "mean_out"),
+                                    _dev(topk_out, "topk_out", torch.int32), ws.data_ptr(), ws.numel(), _stream())
+    _lib.check(st, "sdmoe_expert_mean_topk")
+    return topk_out
+
+
+def colnorm_accum(P, sumsq):
+    """Wanda column statistic (wanda_receiver.py:37-57): sumsq[f] += sum_m (P[m,f] / ||P[m,:]||_2)^2."""
+    lib = _lib.load()
+    pp, ldp = _rows(P, "P")
+    M, F = P.shape
+    if sumsq.numel() != F:
+        raise ValueError(f"colnorm_accum: sumsq has {sumsq.numel()} entries, P has {F} columns")
+    ws = _workspace(P.device)
+    st = lib.sdmoe_colnorm_accum(pp, ldp, M, F, _dev(sumsq, "sumsq", torch.float32), ws.data_ptr(), ws.numel(),
+                                 _stream())
+    _lib.check(st, "sdmoe_colnorm_accum")
+    return sumsq
+
+
+def wanda_mask(W, norm_base, norm_adj, kprune: int, out=None):
+    """modularity/wanda.py:140-160 on device: bit-packed [C, F/8] mask of (top-kprune of |W|*norm_adj per row)
+    AND (|W|*norm_adj > |W|*norm_base); norms fp16 [F]."""
+    lib = _lib.load()
+    wp, ldw = _rows(W, "W")
+    C, F = W.shape
+    if out is None:
+        out = torch.empty((C, F // 8), dtype=torch.uint8, device=W.device)
+    st = lib.sdmoe_wanda_mask(wp, ldw, C, F, _dev(norm_base, "norm_base"), _dev(norm_adj, "norm_adj"), int(kprune),
+                              _dev(out, "bits", torch.uint8), _stream())
+    _lib.check(st, "sdmoe_wanda_mask")
     return out
 
 

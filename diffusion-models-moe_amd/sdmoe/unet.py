@@ -180,6 +180,39 @@ class GEGLU(nn.Module):
         out = out.view(*shp[:-1], self.inner_dim)
         return out, (gate.view(*shp[:-1], self.inner_dim) if want_gate else None)
 
+    def scored(self, x):
+        """Dense GEGLU output (no top-k mask) plus per-token expert scores [tokens, E] fp16 — the arithmetic of
+        GetExperts.hook_fn (neuron_receivers/get_experts.py:50-67). Fused path when eligible (out permuted
+        expert-major, recorded in _out_perm for the down projection)."""
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1])
+        routing = self.routing()
+        act = act_code(self.gelu)
+        self._out_perm = None
+        score = torch.empty((x2.shape[0], routing.E), dtype=torch.float16, device=x.device)
+        if (FUSED_GEGLU and self._allow_permuted_out and self.inner_dim % 80 == 0 and x2.shape[1] % 64 == 0
+                and routing.fusable):
+            w_il, b_il = self._interleaved(routing)
+            out = ops.linear_geglu(x2, w_il, b_il, act, score=score, esize=routing.esize)
+            self._out_perm = (routing, out.data_ptr())
+        else:
+            out = ops.geglu_route(self.proj.run(x2), routing, act, score_out=score, k=routing.E)
+        return out.view(*shp[:-1], self.inner_dim), score
+
+    def dense(self, x):
+        """value * act(gate) in the natural neuron order, ignoring any MoE routing (Wanda discovery,
+        neuron_receivers/wanda_receiver.py:37-57)."""
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1])
+        act = act_code(self.gelu)
+        self._out_perm = None
+        if FUSED_GEGLU and self.inner_dim % 80 == 0 and x2.shape[1] % 64 == 0:
+            w_il, b_il = self._interleaved(None)
+            out = ops.linear_geglu(x2, w_il, b_il, act)
+        else:
+            out = ops.geglu_route(self.proj.run(x2), None, act)
+        return out.view(*shp[:-1], self.inner_dim)
+
     def forward(self, x, scale=1.0):
         if self._sdmoe_deferred and self._forward_hooks:
             return None  # a sdmoe receiver hook computes the routed output (no double compute)

@@ -122,6 +122,29 @@ int sdmoe_linear_geglu(const void* A, long lda, const void* W, long ldw, const v
 int sdmoe_moe_topk_mask(void* P, long ldp, int M, int F, int E, int esize, int k, const void* score,
                         long ld_score, const unsigned* removed_bits, unsigned* sel_out, void* stream);
 
+/*
+ * Skill discovery on the same hook seam.
+ * sdmoe_expert_mean_topk — GetExperts.hook_fn (neuron_receivers/get_experts.py:50-83): mean over tokens of the
+ *   fp16 expert scores [M, E] (score_within_bb.mean(0): fp32 accumulate, one rounding to fp16), restricted to the
+ *   bounding-box positions row_idx[0..n_idx) of every rows_per_img-row image when row_idx != NULL, then the k
+ *   best experts (descending; ties toward the lowest id) into topk_out[k]; mean_out (fp16 [E]) optional.
+ *   E <= 1024. workspace >= ceil(selected rows / 256) * E floats.
+ * sdmoe_colnorm_accum — Wanda.hook_fn (neuron_receivers/wanda_receiver.py:37-57) + ColumnNormCalculator
+ *   (utils.py:321-341): sumsq[f] += sum_m (P[m,f] / max(||P[m,:]||_2, 1e-12))^2 (the squared running column
+ *   norm). workspace >= M + ceil(M / 256) * F floats.
+ * sdmoe_wanda_mask — modularity/wanda.py:140-160: per row n of the down projection W [C, F], metric = fp16(|W| *
+ *   norm) for the base and adjusted prompts (fp16 norms [F]); bit (n, f) = f among the kprune largest adjusted
+ *   metrics of the row (ties toward the lowest column) AND metric_adj > metric_base. bits [C, F/8], the
+ *   bit-packed layout WandaRemoveNeuronsFast consumes. F % 8 == 0, F <= 8192.
+ */
+int sdmoe_expert_mean_topk(const void* score, long ld_score, int M, int E, int rows_per_img, const int* row_idx,
+                           int n_idx, int k, void* mean_out, int* topk_out, float* workspace, long workspace_floats,
+                           void* stream);
+int sdmoe_colnorm_accum(const void* P, long ldp, int M, int F, float* sumsq, float* workspace, long workspace_floats,
+                        void* stream);
+int sdmoe_wanda_mask(const void* W, long ldw, int C, int F, const void* norm_base, const void* norm_adj, int kprune,
+                     void* bits, void* stream);
+
 /* diffusers get_timestep_embedding for one timestep (t_dev if non-NULL, else t), fp16 [dim]. */
 int sdmoe_timestep_embedding(void* out, const float* t_dev, float t, int dim, int flip_sin_to_cos, float freq_shift,
                              void* stream);

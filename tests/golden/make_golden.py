@@ -11,6 +11,8 @@ Covered reference functions:
   * WandaRemoveNeuronsFast.linear_hook_fn neuron_receivers/remove_wanda_neurons_fast.py:69-83, with the real
     Wanda masks of weights_320_1280.csv (the reference's only mask fixture)
   * helper.modify_ffn                    moefication/helper.py:48-62 (labels -> patterns, k)
+  * GetExperts.hook_fn                   neuron_receivers/get_experts.py:50-83 (token-mean expert top-k, bboxes)
+  * Wanda.hook_fn + TimeLayerColumnNorm  neuron_receivers/wanda_receiver.py:37-57, utils.py:321-370
 
 usage: PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
 """
@@ -272,6 +274,69 @@ def gen_counter(pred_mod):
                                                                                                 rec.layer]))]
 
 
+def gen_get_experts(helper, ge_mod):
+    cases = []
+    spec = [  # (C, N, topk, act, dtype, bbox)
+        (320, 32, 0.2, "gelu", torch.float32, None),
+        (320, 32, 0.2, "gelu", torch.float16, None),
+        (640, 16, 0.2, "relu", torch.float16, None),
+        (320, 32, 0.2, "gelu", torch.float16, [0, 3, 5, 17, 31]),
+        (1280, 8, 0.2, "gelu", torch.float32, [1, 2, 6]),
+    ]
+    for i, (C, N, topk, act, dtype, bb) in enumerate(spec):
+        seed = 4000 + i
+        E = 4 * C // 20
+        labels = balanced_labels(4 * C, E, seed)
+        m = make_geglu(C, seed, dtype)
+        if act == "relu":
+            m.gelu = F.relu
+        with tempfile.TemporaryDirectory() as d:
+            path = os.path.join(d, "labels")
+            torch.save(list(map(int, labels)), path)
+            quiet(helper.modify_ffn, m, path, topk)
+        m.bounding_box = bb
+        x = torch.from_numpy(synth.tokens((2, N, C), seed + 1)).to(dtype)
+        name = "ffn0"
+        rec = quiet(ge_mod.GetExperts, 0, 1, 16, {name: E}, [name] * 16)
+        with torch.no_grad():
+            out = rec.hook_fn(m, (x,), None)
+            h, g = m.proj(x).chunk(2, -1)
+            g = m.gelu(g)
+            gb = g if bb is None else g[:, bb, :]
+            mean = torch.matmul(gb.reshape(-1, 4 * C), m.patterns.t()).mean(0)
+        sel = rec.label_counter[0][0]
+        s = torch.sort(mean.float(), descending=True).values
+        tie = bool(m.k < E and s[m.k - 1] == s[m.k])
+        cases.append(dict(
+            name=f"getexperts_C{C}_N{N}_{act}_{str(dtype).split('.')[-1]}{'_bb' if bb else ''}", kind="getexperts",
+            C=C, act=act, dtype=str(dtype).split(".")[-1], k=m.k, E=E, labels=labels, x=x.numpy(), seed=seed,
+            bb=np.array(bb if bb else [], dtype=np.int64), out=out.numpy(), sel=np.array(sel, dtype=np.int64),
+            mean=mean.numpy(), tie=tie, counter_after=np.array([rec.timestep, rec.layer])))
+    return cases
+
+
+def gen_wanda_receiver(w_mod):
+    cases = []
+    for dtype in (torch.float32, torch.float16):
+        C, N, T, L = 320, 16, 2, 2
+        rec = quiet(w_mod.Wanda, 0, T, L)
+        mods = [make_geglu(C, 5000 + l, dtype) for l in range(L)]
+        xs = []
+        with torch.no_grad():
+            for call in range(T * L * 2):  # two "prompts": the statistic accumulates across them
+                if call == T * L:
+                    rec.reset_time_layer()
+                x = torch.from_numpy(synth.tokens((2, N, C), 5100 + call)).to(dtype)
+                xs.append(x.numpy())
+                rec.hook_fn(mods[call % L], (x,), None)
+        norms = rec.predictivity.get_column_norms()
+        cases.append(dict(
+            name=f"wanda_colnorm_C{C}_{str(dtype).split('.')[-1]}", kind="wanda_colnorm", C=C, T=T, L=L,
+            dtype=str(dtype).split(".")[-1], x=np.stack(xs), w_seeds=np.array([5000 + l for l in range(L)]),
+            norms=np.stack([np.stack([norms[t][l].float().numpy() for l in range(L)]) for t in range(T)])))
+    return cases
+
+
 def save(cases):
     index = []
     for c in cases:
@@ -297,7 +362,11 @@ def main():
     moefy = load_ref("neuron_receivers.moefy", "neuron_receivers/moefy.py")
     rem = load_ref("neuron_receivers.remove_skilled_experts", "neuron_receivers/remove_skilled_experts.py")
     wanda = load_ref("neuron_receivers.remove_wanda_neurons_fast", "neuron_receivers/remove_wanda_neurons_fast.py")
+    ge = load_ref("neuron_receivers.get_experts", "neuron_receivers/get_experts.py")
+    load_ref("utils", "utils.py")
+    wr = load_ref("neuron_receivers.wanda_receiver", "neuron_receivers/wanda_receiver.py")
     cases = gen_moefy(helper, moefy) + gen_remove_experts(helper, rem) + gen_wanda(wanda) + gen_counter(pred)
+    cases += gen_get_experts(helper, ge) + gen_wanda_receiver(wr)
     save(cases)
     print(f"wrote {len(cases)} golden cases to {OUT}")
 

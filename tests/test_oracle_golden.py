@@ -132,3 +132,73 @@ def test_counter_golden():
         ctr.update()
     ctr.reset()
     assert (ctr.timestep, ctr.layer) == tuple(c["after_reset"])
+
+
+@pytest.mark.parametrize("name,c", cases("getexperts"), ids=[n for n, _ in cases("getexperts")])
+def test_get_experts_golden(name, c):
+    """GetExperts.hook_fn: dense output bit-exact; top-k of the token-mean score equal as a set unless the
+    reference's k-th/(k+1)-th mean scores tie; counter advanced once."""
+    dt = tdtype(c["dtype"])
+    C = int(c["C"])
+    w, b = synth.geglu_weights(C, int(c["seed"]))
+    w, b = torch.from_numpy(w).to(dt), torch.from_numpy(b).to(dt)
+    P = H.patterns_from_labels(c["labels"], dt)
+    x = torch.from_numpy(c["x"])
+    bb = c["bb"].tolist() or None
+    out, sel, mean = H.get_experts_hook(x, w, b, P, int(c["k"]), str(c["act"]), bb=bb)
+    assert torch.equal(out, torch.from_numpy(c["out"]))
+    ref_mean = torch.from_numpy(c["mean"])
+    # the reference ran on CPU: fp16 mean = fp16(sum) / n (two roundings) vs the device's one rounding
+    tol = 0 if dt == torch.float32 else 2 * float(torch.finfo(torch.float16).eps) * float(ref_mean.abs().max())
+    assert (mean.float() - ref_mean.float()).abs().max().item() <= tol + 1e-6 * float(ref_mean.abs().max())
+    if not bool(c["tie"]):
+        assert set(sel) == set(c["sel"].tolist())
+    assert len(sel) == int(c["k"])
+    assert c["counter_after"].tolist() == [0, 1]
+
+
+@pytest.mark.parametrize("name,c", cases("wanda_colnorm"), ids=[n for n, _ in cases("wanda_colnorm")])
+def test_wanda_colnorm_golden(name, c):
+    """Wanda.hook_fn + TimeLayerColumnNorm over 2 prompts x T x L calls: the oracle's fp32 column norms match
+    the reference's (fp32 exactly up to summation order; fp16 within its rounding of each step)."""
+    dt = tdtype(c["dtype"])
+    C, T, L = int(c["C"]), int(c["T"]), int(c["L"])
+    mods = [tuple(torch.from_numpy(a).to(dt) for a in synth.geglu_weights(C, int(s))) for s in c["w_seeds"]]
+    sums = {}
+    calls = c["x"].shape[0]
+    ctr = H.TimeLayerCounter(L)
+    for i in range(calls):
+        if i == T * L:
+            ctr.reset()
+        x = torch.from_numpy(c["x"][i])
+        w, b = mods[i % L]
+        h, g = torch.nn.functional.linear(x, w, b).chunk(2, -1)
+        out = h * torch.nn.functional.gelu(g)
+        key = (ctr.timestep, ctr.layer)
+        sums[key] = H.column_norm_sumsq(out, sums.get(key))
+        ctr.update()
+    for t in range(T):
+        for l in range(L):
+            ours = sums[(t, l)].sqrt()
+            ref = torch.from_numpy(c["norms"][t][l])
+            rtol = 1e-5 if dt == torch.float32 else 4e-3
+            assert torch.allclose(ours, ref, rtol=rtol, atol=1e-6), (t, l, (ours - ref).abs().max())
+
+
+def test_wanda_mask_restatement_properties():
+    """modularity/wanda.py:140-160 restatement: at most kprune bits per row, every set bit is among the row's
+    kprune largest adjusted metrics and beats the base metric; ties at the boundary go to the lowest column."""
+    g = torch.Generator().manual_seed(0)
+    W = torch.randn(64, 256, generator=g).half()
+    nb = torch.rand(256, generator=g).half()
+    na = torch.rand(256, generator=g).half()
+    m = H.wanda_mask(W, nb, na, 0.05)
+    kp = int(0.05 * 256)
+    assert int(m.sum(1).max()) <= kp
+    ma = (W.abs() * na).float()
+    mb = (W.abs() * nb).float()
+    thr = torch.sort(ma, dim=1, descending=True).values[:, kp - 1:kp]
+    assert bool(((m == 0) | ((ma >= thr) & (ma > mb))).all())
+    # all-equal metrics: the first kprune columns are the selected ones
+    m2 = H.wanda_mask(torch.ones(2, 64).half(), torch.zeros(64).half(), torch.ones(64).half(), 0.25)
+    assert m2[:, :16].all() and not m2[:, 16:].any()

@@ -64,6 +64,14 @@ def main():
         w = (torch.randn(N, K, device=dev) * K ** -0.5).half()
         ms = timeit(lambda: ops.linear(x, w), a.iters)
         rows.append((f"linear M={M} N={N} K={K}", ms, 2.0 * M * N * K / ms / 1e9))
+    # transformer projections with the residual add epilogue (proj_out, to_out): the small-K, HBM-heavy shapes
+    for M, N, K in [(n * 4096, 320, 320), (n * 1024, 640, 640), (n * 256, 1280, 1280), (n * 1024, 1920, 640),
+                    (n * 256, 3840, 1280)]:
+        x = torch.randn(M, K, device=dev).half()
+        w = (torch.randn(N, K, device=dev) * K ** -0.5).half()
+        r = torch.randn(M, N, device=dev).half()
+        ms = timeit(lambda: ops.linear(x, w, residual=r), a.iters)
+        rows.append((f"linear+res M={M} N={N} K={K}", ms, 2.0 * M * N * K / ms / 1e9))
     # fused routed GEGLU: projection GEMM with value*act(gate) + expert-score epilogue, then the top-k mask
     for M, C in [(n * 4096, 320), (n * 1024, 640), (n * 256, 1280)]:
         F, E = 4 * C, C // 5
