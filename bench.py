@@ -42,6 +42,8 @@ def parse():
     p.add_argument("--batch", type=int, default=None,
                    help="prompts per GPU (default 8 = config 4's 64 prompts / 8 GPUs; 2 for sdxl)")
     p.add_argument("--inference-steps", type=int, default=50)
+    p.add_argument("--scheduler", choices=["ddim", "pndm"], default="ddim",
+                   help="ddim: the metric (50 U-Net calls); pndm: the reference's default (51 calls)")
     p.add_argument("--mask", choices=["remove", "union", "none"], default="remove")
     p.add_argument("--topk", type=float, default=0.2)
     p.add_argument("--no-roofline", action="store_true")
@@ -84,11 +86,12 @@ def build(args, world, rank, dev):
     from sdmoe import distributed as D
 
     cfg = UNetConfig.sdxl(128) if args.model == "sdxl" else UNetConfig.sd14(64)
-    pipe = StableDiffusionPipeline.synthetic(cfg, seed=0, device=dev, num_inference_steps=args.inference_steps)
+    pipe = StableDiffusionPipeline.synthetic(cfg, seed=0, device=dev, num_inference_steps=args.inference_steps,
+                                             scheduler=args.scheduler)
     find_and_change_geglu(pipe.unet)                  # relufied U-Net (config 2/3)
     moefy_synthetic(pipe, args.topk, 20, seed=0)      # E = 4C/20 experts, k = int(E*topk)
     geglus = [m for n, m in pipe.unet.named_modules() if n.endswith("ff.net.0")]
-    T = args.inference_steps
+    T = args.inference_steps + (1 if args.scheduler == "pndm" else 0)  # U-Net calls = counter timesteps
     # masks are produced on rank 0 and broadcast once (RCCL); every rank then holds identical device copies
     if args.mask == "none":
         rec = MOEFy(seed=0, store_gates=False)
@@ -296,7 +299,7 @@ def main():
                                    f"{'RemoveExperts skilled-expert mask' if args.mask != 'none' else 'no mask'}"
                                    f"{' + union Wanda mask' if args.mask == 'union' else ''}, "
                                    f"{8 * cfg.sample_size}^2 (4x{cfg.sample_size}x{cfg.sample_size} latents), "
-                                   f"{args.inference_steps} DDIM steps, CFG 7.5",
+                                   f"{args.inference_steps} {args.scheduler.upper()} steps, CFG 7.5",
                        "prompts_per_gpu": args.batch, "global_batch": world * args.batch,
                        "parallelism": f"dp{world}"},
             "step_mfma_frac": round(value / world * TFLOP_PER_IMAGE[args.model] / PEAK_FP16_TFLOPS, 4),

@@ -82,6 +82,51 @@ __global__ void cfg_ddim_kernel(const half_t* __restrict__ eps, long lde, float*
   }
 }
 
+// CFG + one linear multistep update (PNDMScheduler.step_plms, prediction_type "epsilon"):
+//   e   = CFG(eps)                               (stored into history slot `store` when store >= 0)
+//   mo  = c_new * e + sum_j c[j] * hist[j]       (the PLMS combination of the current and past eps)
+//   src = use_cur ? cur : lat ;  if save_cur: cur = lat (before the update)
+//   lat = a * src - b * mo                       (_get_prev_sample: a = sqrt(ap/at), b = (ap - at)/denom)
+// hist: [4][B*4*HW] fp32 NCHW like lat; cur: [B*4*HW] fp32.
+struct MultistepCoef {
+  float c_new, c[4], a, b;
+  int store, use_cur, save_cur;
+};
+
+__global__ void cfg_multistep_kernel(const half_t* __restrict__ eps, long lde, float* __restrict__ lat, int B, int HW,
+                                     int do_cfg, float guidance, float* __restrict__ hist, float* __restrict__ cur,
+                                     MultistepCoef k, half_t* __restrict__ next_in, long ldn) {
+  const long n = (long)B * HW;
+  const long plane = (long)B * 4 * HW;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int b = (int)(i / HW), p = (int)(i % HW);
+    half4 eu = *reinterpret_cast<const half4*>(eps + ((long)b * HW + p) * lde);
+    half4 ec = eu;
+    if (do_cfg) ec = *reinterpret_cast<const half4*>(eps + ((long)(B + b) * HW + p) * lde);
+    half4 nx;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float e = do_cfg ? (float)eu[c] + guidance * ((float)ec[c] - (float)eu[c]) : (float)eu[c];
+      const long li = ((long)b * 4 + c) * HW + p;
+      float mo = k.c_new * e;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (k.c[j] != 0.f) mo += k.c[j] * hist[j * plane + li];
+      if (k.store >= 0) hist[k.store * plane + li] = e;
+      const float x = lat[li];
+      const float src = k.use_cur ? cur[li] : x;
+      if (k.save_cur) cur[li] = x;
+      const float xp = k.a * src - k.b * mo;
+      lat[li] = xp;
+      nx[c] = (half_t)xp;
+    }
+    if (next_in) {
+      *reinterpret_cast<half4*>(next_in + ((long)b * HW + p) * ldn) = nx;
+      if (do_cfg) *reinterpret_cast<half4*>(next_in + ((long)(B + b) * HW + p) * ldn) = nx;
+    }
+  }
+}
+
 __global__ void add_kernel(const half_t* a, const half_t* b, half_t* o, long n8) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
     half8 x = reinterpret_cast<const half8*>(a)[i], y = reinterpret_cast<const half8*>(b)[i], z;
@@ -135,6 +180,26 @@ extern "C" int sdmoe_cfg_ddim_step(const void* eps, long lde, float* lat, int B,
   const long n = (long)B * HW;
   cfg_ddim_kernel<<<grid_for(n), 256, 0, (hipStream_t)stream>>>((const half_t*)eps, lde, lat, B, HW, do_cfg, guidance,
                                                                alpha_t, alpha_prev, (half_t*)next_in, ldn);
+  SDMOE_CHECK_LAUNCH();
+  return SDMOE_OK;
+}
+
+extern "C" int sdmoe_cfg_multistep_step(const void* eps, long lde, float* lat, int B, int HW, int do_cfg,
+                                        float guidance, float* hist, float* cur, const float* coef, const int* flags,
+                                        void* next_in, long ldn, void* stream) {
+  if (!eps || !lat || !hist || !cur || !coef || !flags || B <= 0 || HW <= 0) return SDMOE_EARG;
+  if (lde % 4 || (next_in && ldn % 4)) return SDMOE_ESHAPE;
+  if (flags[0] < -1 || flags[0] > 3) return SDMOE_EARG;
+  MultistepCoef k;
+  k.c_new = coef[0];
+  for (int j = 0; j < 4; ++j) k.c[j] = coef[1 + j];
+  k.a = coef[5];
+  k.b = coef[6];
+  k.store = flags[0];
+  k.use_cur = flags[1];
+  k.save_cur = flags[2];
+  cfg_multistep_kernel<<<grid_for((long)B * HW), 256, 0, (hipStream_t)stream>>>(
+      (const half_t*)eps, lde, lat, B, HW, do_cfg, guidance, hist, cur, k, (half_t*)next_in, ldn);
   SDMOE_CHECK_LAUNCH();
   return SDMOE_OK;
 }

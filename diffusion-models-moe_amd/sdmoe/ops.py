@@ -413,6 +413,26 @@ def cfg_ddim_step(eps: torch.Tensor, lat: torch.Tensor, do_cfg: bool, guidance: 
     return lat
 
 
+def cfg_multistep_step(eps: torch.Tensor, lat: torch.Tensor, do_cfg: bool, guidance: float, hist: torch.Tensor,
+                       cur: torch.Tensor, coef, flags, next_in: torch.Tensor | None = None):
+    """CFG + one PLMS (PNDM) update in place (pipeline.pndm_schedule gives coef[7] / flags[3] per call)."""
+    import ctypes
+    lib = _lib.load()
+    B, C, H, W = lat.shape
+    if tuple(hist.shape) != (4, B, C, H, W) or tuple(cur.shape) != (B, C, H, W):
+        raise ValueError("cfg_multistep_step: history [4, B, 4, H, W] and cur [B, 4, H, W] expected")
+    ep, lde = _rows(eps, "eps")
+    np_, ldn = (None, 0) if next_in is None else _rows(next_in, "next_in")
+    cf = (ctypes.c_float * 7)(*[float(v) for v in coef])
+    fl = (ctypes.c_int * 3)(*[int(v) for v in flags])
+    st = lib.sdmoe_cfg_multistep_step(ep, lde, _dev(lat, "lat", torch.float32), B, H * W, int(bool(do_cfg)),
+                                      float(guidance), _dev(hist, "hist", torch.float32),
+                                      _dev(cur, "cur", torch.float32), ctypes.cast(cf, ctypes.c_void_p),
+                                      ctypes.cast(fl, ctypes.c_void_p), np_, ldn, _stream())
+    _lib.check(st, "sdmoe_cfg_multistep_step")
+    return lat
+
+
 def add(a, b, out=None):
     lib = _lib.load()
     if out is None:

@@ -34,6 +34,55 @@ def ddim_schedule(num_inference_steps=50, num_train_timesteps=1000, beta_start=0
     return [int(t) for t in ts], a_t, a_prev
 
 
+def pndm_schedule(num_inference_steps=50, num_train_timesteps=1000, beta_start=0.00085, beta_end=0.012,
+                  steps_offset=1, set_alpha_to_one=False):
+    """PNDMScheduler(skip_prk_steps=True) as SD-1.x configures it — the reference pipelines' default scheduler
+    (51 U-Net calls for 50 steps, hence the reference's T = 51). Returns, per U-Net call, (timestep, coef[7],
+    flags[3]) for sdmoe_cfg_multistep_step: the PLMS combination of step_plms (diffusers
+    schedulers/scheduling_pndm.py) over a 4-slot eps history ring and _get_prev_sample's a, b."""
+    betas = torch.linspace(beta_start ** 0.5, beta_end ** 0.5, num_train_timesteps, dtype=torch.float32) ** 2
+    ac = torch.cumprod(1.0 - betas, dim=0).double().numpy()
+    final = 1.0 if set_alpha_to_one else float(ac[0])
+    ratio = num_train_timesteps // num_inference_steps
+    ts = (np.arange(0, num_inference_steps) * ratio).round() + steps_offset
+    plms = np.concatenate([ts[:-1], ts[-2:-1], ts[-1:]])[::-1].astype(np.int64)
+    plan, ets, counter = [], [], 0
+    for t_call in plms:
+        timestep, prev_t = int(t_call), int(t_call) - ratio
+        c_hist = [0.0, 0.0, 0.0, 0.0]
+        store, use_cur, save_cur = -1, 0, 0
+        if counter != 1:
+            ets = ets[-3:]
+            store = next(s for s in range(4) if s not in ets)
+            new_ets = ets + [store]
+        else:
+            prev_t, timestep = timestep, timestep + ratio
+            new_ets = ets
+        n = len(new_ets)
+        if n == 1 and counter == 0:
+            c_new, save_cur = 1.0, 1
+        elif n == 1 and counter == 1:
+            c_new, use_cur = 0.5, 1
+            c_hist[new_ets[-1]] = 0.5
+        elif n == 2:
+            c_new = 1.5
+            c_hist[new_ets[-2]] = -0.5
+        elif n == 3:
+            c_new = 23.0 / 12
+            c_hist[new_ets[-2]], c_hist[new_ets[-3]] = -16.0 / 12, 5.0 / 12
+        else:
+            c_new = 55.0 / 24
+            c_hist[new_ets[-2]], c_hist[new_ets[-3]], c_hist[new_ets[-4]] = -59.0 / 24, 37.0 / 24, -9.0 / 24
+        at = float(ac[timestep])
+        ap = float(ac[prev_t]) if prev_t >= 0 else final
+        a = (ap / at) ** 0.5
+        denom = at * (1 - ap) ** 0.5 + (at * (1 - at) * ap) ** 0.5
+        plan.append((int(t_call), [c_new] + c_hist + [a, (ap - at) / denom], [store, use_cur, save_cur]))
+        ets = new_ets
+        counter += 1
+    return plan
+
+
 def prompt_embedding(prompt: str, dim: int = 768) -> torch.Tensor:
     """Seeded synthetic text conditioning [77, dim] fp32 (CPU) standing in for the CLIP text encoder."""
     rng = np.random.default_rng(zlib.crc32(prompt.encode("utf-8")))
@@ -64,7 +113,11 @@ class PipelineOutput:
 
 
 class StableDiffusionPipeline:
-    def __init__(self, unet: UNet2DConditionModel, device="cuda", num_inference_steps=50, guidance_scale=7.5):
+    def __init__(self, unet: UNet2DConditionModel, device="cuda", num_inference_steps=50, guidance_scale=7.5,
+                 scheduler="ddim"):
+        if scheduler not in ("ddim", "pndm"):
+            raise ValueError(f"scheduler must be 'ddim' or 'pndm', got {scheduler!r}")
+        self.scheduler = scheduler  # "pndm": the reference's default (51 U-Net calls per 50 steps)
         self.unet = unet
         self.config = unet.config
         self.device = torch.device(device)
@@ -129,6 +182,13 @@ class StableDiffusionPipeline:
         x_in = torch.zeros((ncopy * B * HW, IN_PAD), dtype=torch.float16, device=self.device)
         eps = torch.empty((ncopy * B * HW, OUT_PAD), dtype=torch.float16, device=self.device)
         ops.prepare_input(lat, x_in, ncopy)
+        if self.scheduler == "pndm":
+            hist = torch.zeros((4,) + tuple(lat.shape), dtype=torch.float32, device=self.device)
+            cur = torch.zeros_like(lat)
+            for t, coef, flags in pndm_schedule(steps):
+                self.unet.forward_nhwc(x_in, float(t), ctx, out=eps, add_hidden=add_hidden)
+                ops.cfg_multistep_step(eps, lat, do_cfg, g, hist, cur, coef, flags, next_in=x_in)
+            return PipelineOutput(images=[lat[i] for i in range(B)])
         ts, a_t, a_prev = ddim_schedule(steps)
         for s, t in enumerate(ts):
             self.unet.forward_nhwc(x_in, float(t), ctx, out=eps, add_hidden=add_hidden)

@@ -165,6 +165,18 @@ int sdmoe_prepare_input(const float* lat, void* out, int B, int HW, long ldo, in
 int sdmoe_cfg_ddim_step(const void* eps, long lde, float* lat, int B, int HW, int do_cfg, float guidance,
                         float alpha_t, float alpha_prev, void* next_in, long ldn, void* stream);
 
+/*
+ * Classifier-free guidance + one linear multistep update of fp32 NCHW latents in place: the PLMS step of
+ * diffusers' PNDMScheduler (skip_prk_steps, prediction_type "epsilon"; SD-1.x's default scheduler, 51 U-Net calls
+ * for 50 steps — the reference's T = 51). Host-computed per step:
+ *   coef[7] = {c_new, c_hist[0..3], a, b}, flags[3] = {store slot (-1 none), use cur, save cur}:
+ *   e = CFG(eps); mo = c_new*e + sum c_hist[j]*hist[j]; hist[store] = e; src = use_cur ? cur : lat;
+ *   if save_cur: cur = lat; lat = a*src - b*mo. hist [4][B*4*HW], cur [B*4*HW] fp32 device buffers.
+ */
+int sdmoe_cfg_multistep_step(const void* eps, long lde, float* lat, int B, int HW, int do_cfg, float guidance,
+                             float* hist, float* cur, const float* coef, const int* flags, void* next_in, long ldn,
+                             void* stream);
+
 /* Tuning knobs for A/B experiments: knob 0 = GEMM LDS pipeline stages (0 auto, 2 or 3); knob 1 = forced GEMM tile
    (0 auto, 1 = 128x160, 2 = 64x160, 3 = 256x320 8-wave, 4 = 256x160 8-wave). */
 int sdmoe_tune(int knob, int value);

@@ -171,15 +171,76 @@ def ddim_schedule(num_inference_steps=50, num_train_timesteps=1000, beta_start=0
     return ts, a_t, a_prev
 
 
+class PNDMRef:
+    """diffusers PNDMScheduler with skip_prk_steps=True (SD-1.x's scheduler config: scaled_linear betas
+    0.00085..0.012, steps_offset 1, set_alpha_to_one False, prediction_type epsilon): set_timesteps + step_plms +
+    _get_prev_sample, restated on tensors (the reference pipelines' default scheduler, utils.py:64-84)."""
+
+    def __init__(self, num_inference_steps=50, num_train_timesteps=1000, beta_start=0.00085, beta_end=0.012,
+                 steps_offset=1, set_alpha_to_one=False):
+        betas = torch.linspace(beta_start ** 0.5, beta_end ** 0.5, num_train_timesteps, dtype=torch.float32) ** 2
+        self.ac = torch.cumprod(1.0 - betas, dim=0).double()
+        self.final = 1.0 if set_alpha_to_one else float(self.ac[0])
+        self.n, self.T = num_inference_steps, num_train_timesteps
+        ts = (np.arange(0, num_inference_steps) * (num_train_timesteps // num_inference_steps)).round()
+        ts = ts + steps_offset
+        self.timesteps = np.concatenate([ts[:-1], ts[-2:-1], ts[-1:]])[::-1].copy().astype(np.int64)
+        self.ets, self.counter, self.cur_sample = [], 0, None
+
+    def prev_sample(self, sample, t, prev_t, mo):
+        at = float(self.ac[t])
+        ap = float(self.ac[prev_t]) if prev_t >= 0 else self.final
+        bt, bp = 1 - at, 1 - ap
+        denom = at * bp ** 0.5 + (at * bt * ap) ** 0.5
+        return (ap / at) ** 0.5 * sample - (ap - at) * mo / denom
+
+    def step(self, mo, timestep, sample):
+        ratio = self.T // self.n
+        prev_t = timestep - ratio
+        if self.counter != 1:
+            self.ets = self.ets[-3:]
+            self.ets.append(mo)
+        else:
+            prev_t = timestep
+            timestep = timestep + ratio
+        if len(self.ets) == 1 and self.counter == 0:
+            mo = mo
+            self.cur_sample = sample
+        elif len(self.ets) == 1 and self.counter == 1:
+            mo = (mo + self.ets[-1]) / 2
+            sample = self.cur_sample
+            self.cur_sample = None
+        elif len(self.ets) == 2:
+            mo = (3 * self.ets[-1] - self.ets[-2]) / 2
+        elif len(self.ets) == 3:
+            mo = (23 * self.ets[-1] - 16 * self.ets[-2] + 5 * self.ets[-3]) / 12
+        else:
+            mo = (1 / 24) * (55 * self.ets[-1] - 59 * self.ets[-2] + 37 * self.ets[-3] - 9 * self.ets[-4])
+        out = self.prev_sample(sample, int(timestep), int(prev_t), mo)
+        self.counter += 1
+        return out
+
+
 def denoise(unet: UNetRef, latents, ctx_uncond, ctx_cond, num_inference_steps=50, guidance_scale=7.5,
-            ff_hook_factory=None, down_hook_factory=None, steps=None, added_cond=None):
+            ff_hook_factory=None, down_hook_factory=None, steps=None, added_cond=None, scheduler="ddim"):
     """StableDiffusionPipeline.__call__'s loop with DDIM + CFG (uncond first). Hook factories take the step
     index and return the (layer, ...) hook for that U-Net call — the reference's (t, l) counter.
     added_cond (SDXL): {"text_embeds": [2B, pooled], "time_ids": [2B, 6]} rows in the [uncond; cond] order."""
-    ts, a_t, a_prev = ddim_schedule(num_inference_steps)
     x = latents.float().clone()
     B = x.shape[0]
     ctx = torch.cat([ctx_uncond, ctx_cond]).float()
+    if scheduler == "pndm":
+        sch = PNDMRef(num_inference_steps)
+        nsteps = len(sch.timesteps) if steps is None else steps
+        for s in range(nsteps):
+            t = int(sch.timesteps[s])
+            ffh = ff_hook_factory(s) if ff_hook_factory else None
+            dh = down_hook_factory(s) if down_hook_factory else None
+            eps = unet(torch.cat([x, x]), float(t), ctx, ff_hook=ffh, down_hook=dh, added_cond=added_cond)
+            eu, ec = eps[:B], eps[B:]
+            x = sch.step(eu + guidance_scale * (ec - eu), t, x).float()
+        return x
+    ts, a_t, a_prev = ddim_schedule(num_inference_steps)
     nsteps = len(ts) if steps is None else steps
     for s in range(nsteps):
         inp = torch.cat([x, x])

@@ -344,3 +344,26 @@ def test_pipeline_fused_geglu_sd14(receiver):
     assert rel_l2(outs[0], outs[1]) <= 2e-2
     ffs = [m for n, m in unet.named_modules() if n.endswith(".ff")]
     assert ffs and all(f._wperm is not None for f in ffs)  # the fused path actually ran
+
+
+def test_pipeline_pndm_remove_experts_tiny(tiny):
+    """The reference's default scheduler: PNDM (skip_prk_steps) = num_inference_steps + 1 U-Net calls, the
+    receiver's (t, l) counter advancing once per call (T = 6 for 5 steps, as T = 51 for 50). RemoveExperts with
+    removal at every call (t < 20) vs the oracle's PNDM restatement, near-tie rows teacher-forced."""
+    from neuron_receivers import GEGLU, RemoveExperts
+    cfg, unet, ref = tiny
+    pipe = StableDiffusionPipeline(unet, DEV, num_inference_steps=5, scheduler="pndm")
+    layers = moefy_tiny(pipe, relu=False)
+    g = torch.Generator().manual_seed(21)
+    T, L = 6, 16
+    lists = {t: {l: sorted(torch.randperm(layers[l][1], generator=g)[:max(1, layers[l][1] // 4)].tolist())
+                 for l in range(L)} for t in range(T)}
+    rec = recording(RemoveExperts)(0, None, T, L, replace_fn=GEGLU, expert_indices=lists, store_gates=False)
+    rec.sels = []
+    out, _ = rec.observe_activation(pipe, ["a harbour at night"])
+    assert (rec.timestep, rec.layer) == (6, 0) and len(rec.sels) == T * L
+    stats = dict(rows=0, clear=0, clear_mismatch=0, forced=0)
+    exp = run_oracle(ref, cfg, ["a harbour at night"], 5, scheduler="pndm",
+                     ff_hook_factory=forced_factory(layers, "gelu", rec.sels, lists, stats))
+    assert stats["clear_mismatch"] == 0, stats
+    assert rel_l2(out[0], exp[0]) <= 1e-2

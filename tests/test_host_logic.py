@@ -254,3 +254,31 @@ def test_oracle_sdxl_micro_conditioning():
     e1 = ref(x, 301.0, ctx, added_cond=ac)
     e2 = ref(x, 301.0, ctx, added_cond={"text_embeds": ac["text_embeds"] * 0, "time_ids": ac["time_ids"]})
     assert torch.isfinite(e1).all() and (e1 - e2).abs().max() > 1e-4
+
+
+def test_pndm_plan_matches_oracle_scheduler():
+    """pipeline.pndm_schedule (the per-call coefficients sdmoe_cfg_multistep_step applies) reproduces the
+    oracle's PNDMScheduler(skip_prk_steps) restatement over all 51 calls, including the duplicated 961 call and
+    the warm-up averaging step; the kernel's update rule is emulated on the host here."""
+    from sdmoe.pipeline import pndm_schedule
+    from oracle.unet_ref import PNDMRef
+    plan = pndm_schedule(50)
+    ref = PNDMRef(50)
+    assert len(plan) == 51 and [p[0] for p in plan] == ref.timesteps.tolist()
+    assert ref.timesteps[:4].tolist() == [981, 961, 961, 941] and ref.timesteps[-1] == 1
+    g = torch.Generator().manual_seed(0)
+    x_ref = torch.randn(2, 4, 8, 8, generator=g, dtype=torch.float64)
+    x = x_ref.clone()
+    hist = torch.zeros((4,) + tuple(x.shape), dtype=torch.float64)
+    cur = torch.zeros_like(x)
+    for t, coef, flags in plan:
+        e = torch.randn(x.shape, generator=g, dtype=torch.float64)
+        x_ref = ref.step(e, t, x_ref)
+        mo = coef[0] * e + sum(coef[1 + j] * hist[j] for j in range(4))
+        if flags[0] >= 0:
+            hist[flags[0]] = e
+        src = cur if flags[1] else x
+        if flags[2]:
+            cur = x.clone()
+        x = coef[5] * src - coef[6] * mo
+    assert torch.allclose(x, x_ref, rtol=1e-10, atol=1e-10)
