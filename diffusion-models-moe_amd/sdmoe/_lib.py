@@ -31,6 +31,8 @@ SIGNATURES = {
     "sdmoe_moe_topk_mask": [_P, _L, _I, _I, _I, _I, _I, _P, _L, _P, _P, _P],
     "sdmoe_timestep_embedding": [_P, _P, _F, _I, _I, _F, _P],
     "sdmoe_cfg_multistep_step": [_P, _L, _P, _I, _I, _I, _F, _P, _P, _P, _P, _P, _L, _P],
+    "sdmoe_sqdist_f32": [_P, _L, _P, _L, _I, _I, _I, _P, _L, _P],
+    "sdmoe_balanced_assign": [_P, _I, _I, ctypes.c_double, _P, _I, _P],
     "sdmoe_expert_mean_topk": [_P, _L, _I, _I, _I, _P, _I, _I, _P, _P, _P, _L, _P],
     "sdmoe_colnorm_accum": [_P, _L, _I, _I, _P, _P, _L, _P],
     "sdmoe_wanda_mask": [_P, _L, _I, _I, _P, _P, _I, _P, _P],

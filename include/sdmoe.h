@@ -145,6 +145,20 @@ int sdmoe_colnorm_accum(const void* P, long ldp, int M, int F, float* sumsq, flo
 int sdmoe_wanda_mask(const void* W, long ldw, int C, int F, const void* norm_base, const void* norm_adj, int kprune,
                      void* bits, void* stream);
 
+/*
+ * Offline MoE-fication: ParamSplit.split (moefication/moe_utils.py:97-107) clusters the
+ * L2-normalised gate rows of each GEGLU with KMeansConstrained(size_min = size_max = expert_size).
+ * sdmoe_sqdist_f32 — D[i][c] = max(|x_i|^2 + |c_c|^2 - 2 x_i.c_c, 0), fp32 device arrays (exact fp32 MFMA
+ *   dot products); X [n, d] (ld ldx), C [k, d] (ld ldc), D [n, k] (ld ldd).
+ * sdmoe_balanced_assign — HOST function: labels[n] minimising sum cost[i][labels[i]] subject to every cluster
+ *   holding exactly n/k points (the min-cost flow of k_means_constrained); cost [n, k] host doubles >= 0.
+ *   Epsilon-scaling auction on integer costs (cost * scale; scale 0 = auto), exact for the integer costs.
+ *   prices [n] (int64, optional) carries the slot prices across calls: warm = 1 starts from them.
+ */
+int sdmoe_sqdist_f32(const float* X, long ldx, const float* C, long ldc, int n, int k, int d, float* D, long ldd,
+                     void* stream);
+int sdmoe_balanced_assign(const double* cost, int n, int k, double scale, int64_t* prices, int warm, int* labels);
+
 /* diffusers get_timestep_embedding for one timestep (t_dev if non-NULL, else t), fp16 [dim]. */
 int sdmoe_timestep_embedding(void* out, const float* t_dev, float t, int dim, int flip_sin_to_cos, float freq_shift,
                              void* stream);

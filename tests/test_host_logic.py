@@ -282,3 +282,41 @@ def test_pndm_plan_matches_oracle_scheduler():
             cur = x.clone()
         x = coef[5] * src - coef[6] * mo
     assert torch.allclose(x, x_ref, rtol=1e-10, atol=1e-10)
+
+
+def test_balanced_assign_native_is_exact():
+    """sdmoe_balanced_assign (host C++ auction; no GPU involved) reaches the exact optimum of the balanced
+    assignment that k_means_constrained solves by min-cost flow: objective equal to scipy's
+    linear_sum_assignment on the slot-expanded cost matrix, every cluster exactly n/k points."""
+    from sdmoe.kmeans import balanced_assign
+    from oracle.kmeans_ref import assign_exact
+    rng = np.random.default_rng(0)
+    for n, k in [(60, 6), (320, 16), (640, 32), (256, 256), (128, 1)]:
+        X = rng.standard_normal((n, 8))
+        C = rng.standard_normal((k, 8))
+        cost = np.sqrt(((X[:, None] - C[None]) ** 2).sum(-1))
+        lab = balanced_assign(cost, k)
+        ref = assign_exact(cost, k)
+        assert np.all(np.bincount(lab, minlength=k) == n // k)
+        assert abs(cost[np.arange(n), lab].sum() - cost[np.arange(n), ref].sum()) <= 1e-9 * n
+        assert np.array_equal(lab, ref)  # continuous random costs: the optimum is unique
+    # integer costs with many ties: the objective is still optimal
+    cost = rng.integers(0, 4, size=(120, 12)).astype(np.float64)
+    lab = balanced_assign(cost, 12)
+    assert cost[np.arange(120), lab].sum() == cost[np.arange(120), assign_exact(cost, 12)].sum()
+
+
+def test_oracle_constrained_kmeans_properties():
+    from oracle.kmeans_ref import constrained_kmeans
+    rng = np.random.default_rng(1)
+    centers = rng.standard_normal((8, 16)) * 4
+    blob = np.repeat(np.arange(8), 10)
+    X = centers[blob] + 0.1 * rng.standard_normal((80, 16))
+    perm = rng.permutation(80)
+    X, blob = X[perm], blob[perm]
+    lab, C, inertia = constrained_kmeans(X, 8, 10, n_init=3)
+    assert np.all(np.bincount(lab, minlength=8) == 10)
+    # well-separated equal-size blobs are recovered exactly (up to cluster ids)
+    for c in range(8):
+        assert len(set(blob[lab == c].tolist())) == 1
+    assert inertia < 80 * 16 * 0.1 ** 2 * 2
