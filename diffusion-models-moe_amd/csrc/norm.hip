@@ -15,6 +15,15 @@ namespace {
 // ref = first element of the group in the image's row 0 (shifted sums keep the variance well conditioned).
 // Reads whole rows with 16-B loads: "virtual thread" vt (NV per thread) owns 8-channel chunk vt % nch and row
 // phase vt / nch, accumulates per-channel sums in registers; LDS reduces phases, then channels per group.
+SDMOE_DEV void gn_accum8(const half8& v, const float (&rf)[8], float (&s1)[8], float (&s2)[8]) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const float a = (float)v[i] - rf[i];
+    s1[i] += a;
+    s2[i] = __builtin_fmaf(a, a, s2[i]);
+  }
+}
+
 template <int NV>
 __global__ __launch_bounds__(256) void gn_partial_kernel(const half_t* __restrict__ X, long ldx, int HW, int C,
                                                          int G, int S, float2* __restrict__ part) {
@@ -36,15 +45,22 @@ __global__ __launch_bounds__(256) void gn_partial_kernel(const half_t* __restric
       float rf[8], s1[8], s2[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) { rf[i] = refs[(c * 8 + i) / cpg]; s1[i] = 0.f; s2[i] = 0.f; }
-      for (int r = r0 + ph; r < r1; r += RP) {
-        half8 v = *reinterpret_cast<const half8*>(base + (long)r * ldx + c * 8);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const float a = (float)v[i] - rf[i];
-          s1[i] += a;
-          s2[i] = __builtin_fmaf(a, a, s2[i]);
-        }
+      // 4 rows' loads in flight per step: the 8x8 / 16x16 latents give a thread only ~8 rows, and one
+      // load-use chain per row left those launches latency-bound (~10 us for 2.6 MB)
+      const half_t* xp = base + (long)(r0 + ph) * ldx + c * 8;
+      const long step = (long)RP * ldx;
+      int r = r0 + ph;
+      for (; r + 3 * RP < r1; r += 4 * RP, xp += 4 * step) {
+        const half8 v0 = *reinterpret_cast<const half8*>(xp);
+        const half8 v1 = *reinterpret_cast<const half8*>(xp + step);
+        const half8 v2 = *reinterpret_cast<const half8*>(xp + 2 * step);
+        const half8 v3 = *reinterpret_cast<const half8*>(xp + 3 * step);
+        gn_accum8(v0, rf, s1, s2);
+        gn_accum8(v1, rf, s1, s2);
+        gn_accum8(v2, rf, s1, s2);
+        gn_accum8(v3, rf, s1, s2);
       }
+      for (; r < r1; r += RP, xp += step) gn_accum8(*reinterpret_cast<const half8*>(xp), rf, s1, s2);
 #pragma unroll
       for (int i = 0; i < 8; ++i) { red[vt][i] = s1[i]; red[vt][8 + i] = s2[i]; }
     }
@@ -98,7 +114,8 @@ __global__ __launch_bounds__(64) void gn_finalize_kernel(const half_t* __restric
   }
 }
 
-// LayerNorm over the last dim (C % 64 == 0, C <= 2048): 8 lanes per row, 8 rows per wave, 32 rows per block;
+// LayerNorm over the last dim (C % 64 == 0, C <= 2048): 8 lanes per row, 8 rows per wave, blockDim/8 rows per
+// block (4 waves; 1 wave when M is small, so the 16x16 / 8x8 latents' few thousand rows still cover every CU);
 // lane (row r = lane/8, sub = lane%8) holds 16-B chunks sub, sub+8, ... (128-B coalesced per 8 lanes), two-pass
 // mean / variance in registers with 8-lane xor reductions.
 template <int CPL>  // chunks per lane = C / 64
@@ -106,7 +123,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const half_t* __restrict
                                                         long ldy, int M, int C, const half_t* __restrict__ gamma,
                                                         const half_t* __restrict__ beta, float eps) {
   const int lane = threadIdx.x & 63, sub = lane & 7;
-  const int row = blockIdx.x * 32 + (threadIdx.x >> 6) * 8 + (lane >> 3);
+  const int row = blockIdx.x * (int)(blockDim.x >> 3) + (int)(threadIdx.x >> 3);
   const bool live = row < M;
   const half_t* xr = X + (long)(live ? row : 0) * ldx;
   half8 v[CPL];
@@ -174,14 +191,16 @@ extern "C" int sdmoe_layernorm(const void* X, long ldx, void* Y, long ldy, int M
   if (M == 0) return SDMOE_OK;
   if (C % 64 || ldx % 8 || ldy % 8 || C > 2048) return SDMOE_ESHAPE;
   hipStream_t s = (hipStream_t)stream;
-  const int blocks = (M + 31) / 32;
+  // 32-row blocks while that still gives >= ~4 blocks per CU, else one-wave 8-row blocks
+  const int nt = M >= 32 * 1024 ? 256 : 64;
+  const int blocks = (M + nt / 8 - 1) / (nt / 8);
   const half_t* x = (const half_t*)X;
   half_t* y = (half_t*)Y;
   const half_t* g = (const half_t*)gamma;
   const half_t* b = (const half_t*)beta;
   switch (C / 64) {
 #define SDMOE_LN(n) \
-    case n: layernorm_kernel<n><<<blocks, 256, 0, s>>>(x, ldx, y, ldy, M, C, g, b, eps); break;
+    case n: layernorm_kernel<n><<<blocks, nt, 0, s>>>(x, ldx, y, ldy, M, C, g, b, eps); break;
     SDMOE_LN(1) SDMOE_LN(2) SDMOE_LN(3) SDMOE_LN(4) SDMOE_LN(5) SDMOE_LN(6) SDMOE_LN(8) SDMOE_LN(10)
     SDMOE_LN(12) SDMOE_LN(16) SDMOE_LN(20) SDMOE_LN(24) SDMOE_LN(32)
 #undef SDMOE_LN

@@ -269,6 +269,20 @@ class Attention(nn.Module):
             self.to_k = LoRACompatibleLinear(self.w_kv.data[:C])
             self.to_v = LoRACompatibleLinear(self.w_kv.data[C:])
         self.to_out = nn.ModuleList([LoRACompatibleLinear(wo, bo), nn.Dropout(0.0)])
+        self._kv_key = None
+        self._kv = None
+
+    def cross_kv(self, ctx2d):
+        """K|V projection of the text context. The context is the same tensor for every denoising step of one
+        pipeline call, so the projection is computed at its first U-Net evaluation and reused by the others
+        (loop-invariant: bit-identical to recomputing it; keyed on the context object, its version and the
+        weights' version, so a new prompt batch or an in-place edit recomputes)."""
+        key = (ctx2d, ctx2d._version, self.w_kv.data_ptr(), self.w_kv._version)
+        k = self._kv_key
+        if k is None or k[0] is not ctx2d or k[1:] != key[1:]:
+            self._kv = ops.linear(ctx2d, self.w_kv)
+            self._kv_key = key
+        return self._kv
 
     def run(self, x2d, nimg, N, residual, ctx2d=None):
         C = x2d.shape[1]
@@ -277,7 +291,7 @@ class Attention(nn.Module):
             a = ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], nimg, N, N, self.heads)
         else:
             q = ops.linear(x2d, self.to_q.weight)
-            kv = ops.linear(ctx2d, self.w_kv)
+            kv = self.cross_kv(ctx2d)
             a = ops.attention(q, kv[:, :C], kv[:, C:], nimg, N, ctx2d.shape[0] // nimg, self.heads)
         return self.to_out[0].run(a, residual=residual)
 
