@@ -5,7 +5,8 @@
 // Layout: Q/K/V/O are read straight out of the projection GEMM outputs ([tokens, heads*D] rows with an
 // arbitrary row stride, so a fused QKV or KV projection needs no split/transposes).
 //
-// Structure (one 256-thread workgroup = 4 waves = 128 queries of one (image, head)):
+// Structure (one 256-thread workgroup = 4 waves x 16*NQF queries of one (image, head); NQF = 2 by default, 4 on
+// request -- it amortises every K/V LDS read and LDS-DMA piece over 64 queries per wave, but measured no faster):
 //   * "swapped" product S^T = K Q^T with v_mfma_f32_16x16x32_f16: the query sits on the MFMA lane, so the
 //     running max / sum / output rescale of the online softmax are lane-local (two shuffles per tile for
 //     the max only; the row sum is kept as lane partials and combined once at the end);
@@ -54,7 +55,7 @@ SDMOE_DEV void bld16(__amdgpu_buffer_rsrc_t rs, const half_t* lds_dst, unsigned 
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)lds_dst, 16, voff, 0, 0, 0);
 }
 
-template <int D>
+template <int D, int NQF>
 __global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn_fwd_kernel(AttnParams p) {
   constexpr int DK = ((D + 31) / 32) * 32;   // contraction dim padded for 16x16x32
   constexpr int DV = ((D + 15) / 16) * 16;   // output dim padded to 16-row fragments
@@ -88,7 +89,7 @@ __global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn_fwd_kernel(AttnP
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, w = lane & 15;
   const int b = blockIdx.z, h = blockIdx.y;
-  const int q0 = blockIdx.x * 128 + wave * 32;
+  const int q0 = blockIdx.x * (64 * NQF) + wave * (16 * NQF);
 
   const half_t* Qb = p.Q + (long)b * p.Nq * p.ldq + h * D;
   const half_t* Kb = p.K + (long)b * p.Nk * p.ldk + h * D;
@@ -130,9 +131,9 @@ __global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn_fwd_kernel(AttnP
 
   // Q fragments (B operand of S^T = K Q^T), pre-multiplied by scale*log2(e) so that the score accumulator is
   // already the exp2 argument: lane holds Q[q = w][d = 32c + 8g + j]
-  half8 qf[2][NDC];
+  half8 qf[NQF][NDC];
 #pragma unroll
-  for (int f = 0; f < 2; ++f)
+  for (int f = 0; f < NQF; ++f)
 #pragma unroll
     for (int c = 0; c < NDC; ++c) {
       const int q = q0 + f * 16 + w, d = 32 * c + 8 * g;
@@ -143,12 +144,14 @@ __global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn_fwd_kernel(AttnP
       qf[f][c] = v;
     }
 
-  float4v oacc[2][NDF];
+  float4v oacc[NQF][NDF];
 #pragma unroll
-  for (int f = 0; f < 2; ++f)
+  for (int f = 0; f < NQF; ++f)
 #pragma unroll
     for (int d = 0; d < NDF; ++d) oacc[f][d] = (float4v){0.f, 0.f, 0.f, 0.f};
-  float mrun[2] = {0.f, 0.f}, lrun[2] = {0.f, 0.f};
+  float mrun[NQF], lrun[NQF];
+#pragma unroll
+  for (int f = 0; f < NQF; ++f) mrun[f] = lrun[f] = 0.f;
 
   // V^T fragment addresses (tr reads, key slots permuted to match P); lanes of the ones-column group read the
   // constant block instead
@@ -172,9 +175,9 @@ __global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn_fwd_kernel(AttnP
 
     // ---- S'^T = K Q~^T - m: the accumulator starts at -m (running max, log2 units), so after the MFMAs it
     //      holds exp2's argument directly (tile 0 starts at 0 and sets m from its own max)
-    float4v s[2][4];
+    float4v s[NQF][4];
 #pragma unroll
-    for (int f = 0; f < 2; ++f) {
+    for (int f = 0; f < NQF; ++f) {
       const float nm = -mrun[f];
 #pragma unroll
       for (int kf = 0; kf < 4; ++kf) s[f][kf] = (float4v){nm, nm, nm, nm};
@@ -185,15 +188,15 @@ __global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn_fwd_kernel(AttnP
       for (int c = 0; c < NDC; ++c) {
         half8 a = *reinterpret_cast<const half8*>(Kt + (kf * 16 + w) * RS + 32 * c + 8 * g);
 #pragma unroll
-        for (int f = 0; f < 2; ++f) s[f][kf] = mfma16x16x32(a, qf[f][c], s[f][kf]);
+        for (int f = 0; f < NQF; ++f) s[f][kf] = mfma16x16x32(a, qf[f][c], s[f][kf]);
       }
 
     // ---- online softmax (query on the lane), VALU-lean: per score one exp2, a third of a max3 and half a
     //      cvt_pk; deferred rescale (m moves only when a tile max exceeds it by > RESCALE_THR, log2 units, so
     //      p <= 2^8 stays well inside fp16); masking only in the peeled ragged last tile
-    half8 pb[2][2];
+    half8 pb[NQF][2];
 #pragma unroll
-    for (int f = 0; f < 2; ++f) {
+    for (int f = 0; f < NQF; ++f) {
       if constexpr (RAGGED) {
 #pragma unroll
         for (int kf = 0; kf < 4; ++kf)
@@ -254,7 +257,7 @@ __global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn_fwd_kernel(AttnP
         half4 hi = ds_read_tr(vaddr(Vt, c2, 1, df));
         half8 a = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 #pragma unroll
-        for (int f = 0; f < 2; ++f) oacc[f][df] = mfma16x16x32(a, pb[f][c2], oacc[f][df]);
+        for (int f = 0; f < NQF; ++f) oacc[f][df] = mfma16x16x32(a, pb[f][c2], oacc[f][df]);
       }
 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of tile kt+1 have landed
@@ -280,7 +283,7 @@ __global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn_fwd_kernel(AttnP
   // ---- normalise and store O[q][d] (lane: query w, rows d = 16df + 4g + i)
   half_t* Ob = p.O + (long)b * p.Nq * p.ldo + h * D;
 #pragma unroll
-  for (int f = 0; f < 2; ++f) {
+  for (int f = 0; f < NQF; ++f) {
     float l;
     if (SUM_BY_MFMA) {
       // O^T row D (df = D/16, lane group g = (D%16)/4, register D%4) holds sum_k P[k][q]; broadcast to all g
@@ -306,15 +309,33 @@ __global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn_fwd_kernel(AttnP
   }
 }
 
+int g_attn_nqf = 0;  // sdmoe_tune knob 4: query fragments per wave (0 = auto, 2 or 4)
+
 template <int D>
 int launch(const AttnParams& p, int nimg, hipStream_t s) {
-  dim3 grid((p.Nq + 127) / 128, p.heads, nimg);
-  attn_fwd_kernel<D><<<grid, 256, 0, s>>>(p);
+  // 64 queries per wave (NQF = 4) only on request (knob 4): at d = 40, N = 4096 it measured equal to NQF = 2
+  // (500 us both; 232 vs 128 VGPRs halves the waves per SIMD) and 12 % slower on the 77-key cross-attention;
+  // head dims above 40 would spill at NQF = 4 (64: 16 VGPRs, 80: 130)
+  constexpr bool WIDE_OK = D <= 40;
+  const bool wide = g_attn_nqf == 4;
+  if (WIDE_OK && wide) {
+    dim3 grid((p.Nq + 255) / 256, p.heads, nimg);
+    attn_fwd_kernel<D, (WIDE_OK ? 4 : 2)><<<grid, 256, 0, s>>>(p);
+  } else {
+    dim3 grid((p.Nq + 127) / 128, p.heads, nimg);
+    attn_fwd_kernel<D, 2><<<grid, 256, 0, s>>>(p);
+  }
   SDMOE_CHECK_LAUNCH();
   return SDMOE_OK;
 }
 
 }  // namespace
+
+int sdmoe_attn_set_nqf(int v) {
+  if (v != 0 && v != 2 && v != 4) return SDMOE_EARG;
+  g_attn_nqf = v;
+  return SDMOE_OK;
+}
 
 extern "C" int sdmoe_attention(const void* Q, long ldq, const void* K, long ldk, const void* V, long ldv,
                                void* O, long ldo, int nimg, int Nq, int Nk, int heads, int head_dim,

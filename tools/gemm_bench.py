@@ -34,12 +34,14 @@ def main():
     ap.add_argument("--only", default="", help="run only rows whose label contains this")
     ap.add_argument("--bk", type=int, default=0, help="GEMM K-step depth (sdmoe_tune knob 2), 0 = auto")
     ap.add_argument("--prio", type=int, default=0, help="s_setprio around the MFMA block (knob 3)")
+    ap.add_argument("--nqf", type=int, default=0, help="attention query fragments per wave (knob 4), 0 = auto")
     a = ap.parse_args()
     from sdmoe import _lib
     _lib.check(_lib.load().sdmoe_tune(0, a.stages), "tune")
     _lib.check(_lib.load().sdmoe_tune(1, a.tile), "tune")
     _lib.check(_lib.load().sdmoe_tune(2, a.bk), "tune")
     _lib.check(_lib.load().sdmoe_tune(3, a.prio), "tune")
+    _lib.check(_lib.load().sdmoe_tune(4, a.nqf), "tune")
     print("stages", a.stages, "tile", a.tile, "bk", a.bk)
     n = a.nimg
     dev = "cuda"
