@@ -46,6 +46,9 @@ def parse():
                    help="ddim: the metric (50 U-Net calls); pndm: the reference's default (51 calls)")
     p.add_argument("--mask", choices=["remove", "union", "none"], default="remove")
     p.add_argument("--topk", type=float, default=0.2)
+    p.add_argument("--topk-mask", choices=["down", "pass"], default="down",
+                   help="down: the top-k mask is applied by the down projection as it reads the GEGLU product "
+                        "(sdmoe_linear_keep); pass: a separate masking pass over the product (A/B reference)")
     p.add_argument("--no-roofline", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-evals", type=int, default=2, help="CPU oracle U-Net evaluations to time")
@@ -222,7 +225,9 @@ def main():
     world, rank, local = setup_dist(args.gpus)
     dev = f"cuda:{local}" if world > 1 else "cuda:0"
     from sdmoe import ops, _lib
+    import sdmoe.unet as U
     _lib.load()
+    U.FUSED_KEEP = args.topk_mask == "down"
     cfg, pipe, rec, wanda = build(args, world, rank, dev)
     # global prompt list: rank r takes its contiguous shard (per-prompt seeds use the global index)
     from sdmoe import distributed as D

@@ -51,6 +51,10 @@ struct GemmParams {
   half_t* score; long ld_score;
   int esize;
   int prio;  // experiment knob: raise wave priority around the MFMA block
+  // expert keep mask of the A operand (MODE_KEEP): keep[(k / 64) * M * 8 + m * 8 + (k % 64) / 8] bit (k % 8) =
+  // neuron k of token m survives the top-k; the A fragments are ANDed with it after their LDS read
+  const uint8_t* keep;
+  int keep_bytes;
 };
 
 SDMOE_DEV int swz(int row) { return (row >> 1) & 7; }
@@ -89,7 +93,14 @@ SDMOE_DEV void epilogue8(const GemmParams& p, int m, int n, float (&v)[8]) {
   *reinterpret_cast<half8*>(p.C + (long)m * p.ldc + n) = o;
 }
 
-enum { MODE_GEMM = 0, MODE_CONV = 1, MODE_CONV_UP = 2, MODE_GEGLU = 3 };  // GEGLU: GEMM loads, routed-GEGLU epilogue
+// GEGLU: GEMM loads, routed-GEGLU epilogue; KEEP: GEMM whose A operand is masked per (row, neuron) by keep bits
+enum { MODE_GEMM = 0, MODE_CONV = 1, MODE_CONV_UP = 2, MODE_GEGLU = 3, MODE_KEEP = 4 };
+
+// LDS bytes one ring stage holds besides the A/B tiles: the keep bytes of the tile's rows for one 64-deep K-step
+// (MODE_KEEP: BM rows x 8 bytes, whole 1-KiB LDS-DMA pieces)
+template <int BM, int MODE>
+constexpr int keep_stage_bytes() { return MODE == MODE_KEEP ? ((BM * 8 + 1023) / 1024) * 1024 : 0; }
+constexpr int KEEP_LUT_BYTES = 16 * 8;  // 4 keep bits -> 4 x 16-bit lane masks
 
 // Routed-GEGLU epilogue over one staged pass (rows x WN fp32 in LDS, row stride WN_PAD) of a wave's tile
 // whose columns n0..n0+WN-1 are [value 8 | gate 8] chunk pairs. Rounds exactly like the unfused path
@@ -178,21 +189,29 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
   auto swzk = [](int row) { return (row >> 1) & (CPRW - 1); };  // conflict-free b128 fragment reads
   constexpr bool CONV = MODE == MODE_CONV || MODE == MODE_CONV_UP;
   constexpr bool GEGLU = MODE == MODE_GEGLU;
+  constexpr bool KEEP = MODE == MODE_KEEP;
+  static_assert(!KEEP || BKT == 64, "keep bytes are laid out per 64-deep K-step");
   constexpr int NW = WMW * WNW;                  // waves per workgroup
   constexpr int WM = BM / WMW, WN = BN / WNW;    // per-wave output tile
   constexpr int FM = WM / 16, FN = WN / 16;
   static_assert(WM % 16 == 0 && WN % 16 == 0, "wave tile must be whole 16x16 fragments");
   constexpr int A_INS = BM / RPP, B_INS = BN / RPP;  // 1-KiB LDS-DMA wave-instructions per stage
   constexpr int A_PW = (A_INS + NW - 1) / NW, B_PW = (B_INS + NW - 1) / NW;
-  constexpr int PER_WAVE = A_PW + B_PW;          // every wave issues exactly this many (surplus -> dummy slot)
+  constexpr int K_INS = keep_stage_bytes<BM, MODE>() / 1024;  // keep pieces per stage (<= NW)
+  static_assert(K_INS <= NW, "one keep piece per wave at most");
+  constexpr int K_PW = KEEP ? 1 : 0;             // every wave issues one (waves >= K_INS repeat piece 0)
+  constexpr int PER_WAVE = A_PW + B_PW + K_PW;   // every wave issues exactly this many (surplus -> dummy slot)
   constexpr int STAGE_AB = (BM + BN) * BK * 2;
   constexpr bool PADDED = (A_PW * NW != A_INS) || (B_PW * NW != B_INS);
-  constexpr int STAGE = STAGE_AB + (PADDED ? 1024 : 0);
+  constexpr int KEEP_OFF = STAGE_AB + (PADDED ? 1024 : 0);
+  constexpr int STAGE = KEEP_OFF + keep_stage_bytes<BM, MODE>();
   constexpr int WN_PAD = WN + 4;
   constexpr int NPASS = (NW * (WM / 2) * WN_PAD * 4 <= NSTAGE * STAGE) ? 2 : ((NW * (WM / 4) * WN_PAD * 4 <= NSTAGE * STAGE) ? 4 : 8);
   static_assert(FM % NPASS == 0, "epilogue passes must split the wave's fragment rows");
   constexpr int EPI = NW * (WM / NPASS) * WN_PAD * 4;
-  constexpr int SMEM = (NSTAGE * STAGE > EPI) ? NSTAGE * STAGE : EPI;
+  constexpr int SMEM0 = (NSTAGE * STAGE > EPI) ? NSTAGE * STAGE : EPI;
+  constexpr int LUT_OFF = SMEM0;                 // MODE_KEEP: 16-entry nibble -> lane-mask table behind everything
+  constexpr int SMEM = SMEM0 + (KEEP ? KEEP_LUT_BYTES : 0);
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -254,6 +273,25 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
     bvoff[j] = (j * NW + wave < B_INS && n < p.N) ? (unsigned)((long)n * p.ldw * 2) + (unsigned)((lch ^ swzk(r)) * 16)
                                                   : OOB;
   }
+  // keep pieces (MODE_KEEP): wave w < K_INS stages the keep bytes of tile rows [128 w, 128 w + 128) (16 B = two rows
+  // per lane); the other waves repeat piece 0 -- the same bytes to the same LDS place -- so every wave issues
+  // PER_WAVE instructions per stage and the counted vmcnt waits stay uniform
+  const __amdgpu_buffer_rsrc_t rsK =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.keep, (short)0, KEEP ? p.keep_bytes : 0, 0x00020000);
+  unsigned kvoff = OOB;
+  int kdst = KEEP_OFF;
+  if constexpr (KEEP) {
+    const int piece = wave < K_INS ? wave : 0;
+    kvoff = (unsigned)((m0 + 128 * piece) * 8 + lane * 16);
+    kdst = KEEP_OFF + piece * 1024;
+    // nibble -> two 16-bit-lane masks: entry e masks halves 0..3 by bits 0..3 of e
+    if (tid < 16) {
+      const unsigned lo = ((tid & 1) ? 0xFFFFu : 0u) | ((tid & 2) ? 0xFFFF0000u : 0u);
+      const unsigned hi = ((tid & 4) ? 0xFFFFu : 0u) | ((tid & 8) ? 0xFFFF0000u : 0u);
+      *reinterpret_cast<uint2v*>(smem + LUT_OFF + tid * 8) = (uint2v){lo, hi};
+    }
+    __syncthreads();  // no LDS-DMA in flight yet
+  }
   // LDS destination of wave-instruction j (surplus instructions of a padded tile land in a dummy 1-KiB slot)
   auto a_dst = [&](int j) { return (j * NW + wave < A_INS) ? (j * NW + wave) * 1024 : STAGE_AB; };
   auto b_dst = [&](int j) { return (j * NW + wave < B_INS) ? BM * BK * 2 + (j * NW + wave) * 1024 : STAGE_AB; };
@@ -295,6 +333,7 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
     }
 #pragma unroll
     for (int j = 0; j < B_PW; ++j) bld16(rsW, sa + b_dst(j), bvoff[j], kb);
+    if constexpr (KEEP) bld16(rsK, sa + kdst, kvoff, (unsigned)ks * (unsigned)p.M * 8u);
   };
 
   float4v acc[FM][FN];
@@ -336,6 +375,14 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
       for (int i = 0; i < FM; ++i) {
         const int row = wr * WM + i * 16 + fr;
         af[i] = *reinterpret_cast<const half8*>(sa + row * RB + (((kk * 4 + fg) ^ swzk(row)) << 4));
+        if constexpr (KEEP) {  // zero the neurons of this row's dropped experts (8 neurons = chunk kk*4+fg)
+          const unsigned kbyte = *reinterpret_cast<const unsigned char*>(sa + KEEP_OFF + row * 8 + kk * 4 + fg);
+          const uint2v lo = *reinterpret_cast<const uint2v*>(smem + LUT_OFF + (kbyte & 15u) * 8);
+          const uint2v hi = *reinterpret_cast<const uint2v*>(smem + LUT_OFF + (kbyte >> 4) * 8);
+          uint4v u = __builtin_bit_cast(uint4v, af[i]);
+          u[0] &= lo[0]; u[1] &= lo[1]; u[2] &= hi[0]; u[3] &= hi[1];
+          af[i] = __builtin_bit_cast(half8, u);
+        }
       }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
@@ -436,7 +483,8 @@ int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
     // 4-wave tiles: 2-stage ring (2 workgroups/CU) when the grid has >= ~300 workgroups, else 3-stage; 8-wave
     // tiles: 3-stage where it fits in LDS -- measured crossovers on MI355X.
     const int stages = g_stages ? g_stages : ((WMW * WNW == 4 && ntiles * p.ksplit >= 300) ? 2 : 3);
-    constexpr bool FITS3 = 3 * ((BM + BN) * 64 * 2 + 1024) <= 160 * 1024;
+    constexpr bool FITS3 = 3 * ((BM + BN) * 64 * 2 + 1024 + keep_stage_bytes<BM, MODE>()) +
+                               (MODE == MODE_KEEP ? KEEP_LUT_BYTES : 0) <= 160 * 1024;
     if constexpr (FITS3) {
       if (stages == 2) gemm_kernel<BM, BN, WMW, WNW, MODE, 2, 64><<<grid, NT, 0, s>>>(p);
       else gemm_kernel<BM, BN, WMW, WNW, MODE, 3, 64><<<grid, NT, 0, s>>>(p);
@@ -567,6 +615,23 @@ extern "C" int sdmoe_linear(const void* A, long lda, const void* W, long ldw, co
   if (ab >= (long)OOB || wb >= (long)OOB) return SDMOE_ESHAPE;
   p.a_bytes = (int)ab; p.w_bytes = (int)wb;
   return dispatch<MODE_GEMM>(p, workspace, workspace_floats, (hipStream_t)stream);
+}
+
+extern "C" int sdmoe_linear_keep(const void* A, long lda, const void* keep, const void* W, long ldw, const void* bias,
+                                 const void* R, long ldr, void* C, long ldc, int M, int N, int K, float* workspace,
+                                 long workspace_floats, void* stream) {
+  if (!A || !keep || !W || !C || M < 0 || N <= 0 || K <= 0) return SDMOE_EARG;
+  if (M == 0) return SDMOE_OK;
+  if (K % 64 || N % 8 || lda % 8 || ldw % 8 || ldc % 8 || (R && ldr % 8)) return SDMOE_ESHAPE;
+  GemmParams p{};
+  p.A = (const half_t*)A; p.lda = lda; p.W = (const half_t*)W; p.ldw = ldw;
+  p.bias = (const half_t*)bias; p.R = (const half_t*)R; p.ldr = ldr; p.C = (half_t*)C; p.ldc = ldc;
+  p.M = M; p.N = N; p.K = K; p.act = ACT_NONE; p.rows_per_batch = 1;
+  const long ab = ((long)(M - 1) * lda + K) * 2, wb = ((long)(N - 1) * ldw + K) * 2, kb = (long)(K / 64) * M * 8;
+  if (ab >= (long)OOB || wb >= (long)OOB || kb >= (long)OOB) return SDMOE_ESHAPE;
+  p.a_bytes = (int)ab; p.w_bytes = (int)wb;
+  p.keep = (const uint8_t*)keep; p.keep_bytes = (int)kb;
+  return dispatch<MODE_KEEP>(p, workspace, workspace_floats, (hipStream_t)stream);
 }
 
 extern "C" int sdmoe_linear_geglu(const void* A, long lda, const void* W, long ldw, const void* bias, void* P,

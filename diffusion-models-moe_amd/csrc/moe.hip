@@ -142,98 +142,156 @@ __global__ __launch_bounds__(256) void geglu_route_kernel(RouteParams p) {
 
 // Top-k expert mask over a routed-GEGLU product computed by sdmoe_linear_geglu (experts contiguous, esize
 // neurons each): per token, scores (fp16, removed experts -> 0) -> the same radix top-k as above -> zero the
-// neurons of every expert that is not selected (or is removed). One wave per token; only zeros are written.
-template <int SLOTS, int SC>  // SC: compile-time expert size (0 = runtime S)
-__global__ __launch_bounds__(256) void moe_topk_mask_kernel(half_t* __restrict__ P, long ldp, int M, int F, int E,
-                                                            int S_, int k, const half_t* __restrict__ score,
-                                                            long lds, const uint32_t* __restrict__ removed,
-                                                            uint32_t* __restrict__ sel_out) {
-  __shared__ uint32_t selw_all[4][8];
+// neurons of every expert that is not selected (or is removed). One wave per TPW tokens: the TPW score rows are
+// loaded up front (one 128-B row per token and wave left the kernel latency-bound: ~30 us for 65536 tokens), then
+// selected one after the other; only zeros are written.
+// KEEPOUT: P is left alone; the kept neurons are written as keep bits for the down projection to apply to its
+// A operand (sdmoe_linear_keep): keep[(n / 64) * M + m] bit n % 64, one 64-bit word per token and 64-neuron
+// K-step, staged in LDS so each K-step's 16 words of the workgroup's tokens leave as one whole 128-B line.
+struct Slots64 {  // per-slot 64-bit expert masks (slot i = experts 64 i .. 64 i + 63)
+  unsigned long long a = 0, b = 0, c = 0, d = 0;
+  SDMOE_DEV void set(int i, unsigned long long v) {
+    if (i == 0) a = v; else if (i == 1) b = v; else if (i == 2) c = v; else d = v;
+  }
+  SDMOE_DEV unsigned long long get(int i) const { return i == 0 ? a : (i == 1 ? b : (i == 2 ? c : d)); }
+};
+
+template <int SLOTS, int SC, bool KEEPOUT>  // SC: compile-time expert size (0 = runtime S)
+__global__ __launch_bounds__(256) void moe_topk_mask_kernel(
+    half_t* __restrict__ P, long ldp, int M, int F, int E, int S_, int k, const half_t* __restrict__ score, long lds,
+    const uint32_t* __restrict__ removed, uint32_t* __restrict__ sel_out, unsigned long long* __restrict__ keep) {
+  constexpr int TPW = 4;                        // tokens per wave
+  constexpr int WPB = 4;                        // waves per workgroup
+  constexpr int TPB = TPW * WPB;                // tokens per workgroup
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t* selw = selw_all[wave];
   const int S = SC ? SC : S_;
-  const int m = blockIdx.x * 4 + wave;
-  if (m >= M) return;  // wave-uniform; no block-level barrier below
+  const int mw = blockIdx.x * TPB + wave * TPW;  // first token of this wave
+  if (!KEEPOUT && mw >= M) return;  // wave-uniform; the mask form has no block-level barrier below
   const int nw = (E + 31) >> 5;
-  uint32_t key[SLOTS];
+  // the TPW score rows first, all loads in flight before anything waits on them (unconditional loads at clamped
+  // indices: a per-lane validity branch around each load made the compiler wait for each separately), then the
+  // removed bits; separate row arrays keep every index constant
+  half_t sc0[SLOTS], sc1[SLOTS], sc2[SLOTS], sc3[SLOTS];
+  static_assert(TPW == 4, "four score rows per wave");
+  auto load_row = [&](half_t (&dst)[SLOTS], int t) {
+    const half_t* srow = score + (long)min(mw + t, M - 1) * lds;
+#pragma unroll
+    for (int i = 0; i < SLOTS; ++i) dst[i] = srow[min(lane + 64 * i, E - 1)];
+  };
+  load_row(sc0, 0);
+  load_row(sc1, 1);
+  load_row(sc2, 2);
+  load_row(sc3, 3);
+  uint32_t rmw[SLOTS];  // removed bits of this lane's experts
   bool valid[SLOTS];
 #pragma unroll
   for (int i = 0; i < SLOTS; ++i) {
     const int e = lane + 64 * i;
     valid[i] = e < E;
-    half_t sc = valid[i] ? score[(long)m * lds + e] : (half_t)0.f;
-    if (valid[i] && removed && ((removed[e >> 5] >> (e & 31)) & 1u)) sc = (half_t)0.f;
-    key[i] = valid[i] ? order_key(sc) : 0u;
+    const uint32_t r = removed ? (removed[min(e, E - 1) >> 5] >> (e & 31)) & 1u : 0u;
+    rmw[i] = valid[i] ? r : 0u;
   }
-  uint32_t T = 0;
-  for (int bit = 15; bit >= 0; --bit) {
-    const uint32_t cand = T | (1u << bit);
-    int cnt = 0;
-#pragma unroll
-    for (int i = 0; i < SLOTS; ++i) cnt += __popcll(__ballot(valid[i] && key[i] >= cand));
-    if (cnt >= k) T = cand;
-  }
-  int gt = 0;
-#pragma unroll
-  for (int i = 0; i < SLOTS; ++i) gt += __popcll(__ballot(valid[i] && key[i] > T));
-  const int need = k - gt;
   const unsigned long long below = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
-  int rank_base = 0;
+  // KEEPOUT: [TPB][F/64 + 1] words in dynamic LDS (16 tokens x 8 B = one whole 128-B line per K-step)
+  extern __shared__ unsigned long long kw_dyn[];
+  const int kws = (F >> 6) + 1;
+
+  auto process = [&](const half_t (&scr)[SLOTS], int t) {
+    const int m = mw + t;
+    const bool live = m < M;
+    uint32_t key[SLOTS];
 #pragma unroll
-  for (int i = 0; i < SLOTS; ++i) {
-    const bool tie = valid[i] && key[i] == T;
-    const unsigned long long tm = __ballot(tie);
-    const bool sel = k > 0 && valid[i] && (key[i] > T || (tie && rank_base + __popcll(tm & below) < need));
-    rank_base += __popcll(tm);
-    const unsigned long long sm = __ballot(sel);
-    if (lane == 0) {
-      if (2 * i < 8) selw[2 * i] = (uint32_t)sm;
-      if (2 * i + 1 < 8) selw[2 * i + 1] = (uint32_t)(sm >> 32);
+    for (int i = 0; i < SLOTS; ++i) key[i] = valid[i] ? order_key(rmw[i] ? (half_t)0.f : scr[i]) : 0u;
+    uint32_t T = 0;
+    for (int bit = 15; bit >= 0; --bit) {
+      const uint32_t cand = T | (1u << bit);
+      int cnt = 0;
+#pragma unroll
+      for (int i = 0; i < SLOTS; ++i) cnt += __popcll(__ballot(valid[i] && key[i] >= cand));
+      if (cnt >= k) T = cand;
     }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  if (sel_out && lane < nw) sel_out[(long)m * nw + lane] = selw[lane];
-  uint32_t keepw[8];
+    int gt = 0;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) keepw[i] = (i < nw) ? selw[i] & (removed ? ~removed[i] : ~0u) : 0u;
-  half_t* row = P + (long)m * ldp;
-  for (int c = lane; c < (F >> 3); c += 64) {
-    unsigned kb = 0;  // keep bit per neuron of this 8-neuron chunk
+    for (int i = 0; i < SLOTS; ++i) gt += __popcll(__ballot(valid[i] && key[i] > T));
+    const int need = k - gt;
+    // selection and kept experts (selected, not removed) as wave-uniform ballots: bit e & 63 of slot e >> 6. They
+    // stay in registers -- no lane reads a word another lane wrote to LDS
+    // (four named scalars, not an array: a select chain over array elements is folded back into a dynamically
+    //  indexed private array, i.e. scratch)
+    int rank_base = 0;
+    Slots64 sel_sl, keep_sl;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int e = (8 * c + j) / S;
-      kb |= ((keepw[e >> 5] >> (e & 31)) & 1u) << j;
+    for (int i = 0; i < SLOTS; ++i) {
+      const bool tie = valid[i] && key[i] == T;
+      const unsigned long long tm = __ballot(tie);
+      const bool sel = k > 0 && valid[i] && (key[i] > T || (tie && rank_base + __popcll(tm & below) < need));
+      rank_base += __popcll(tm);
+      sel_sl.set(i, __ballot(sel));
+      keep_sl.set(i, __ballot(sel && !rmw[i]));
     }
-    if (kb == 0xffu) continue;
-    half8 v = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (kb) {
-      v = *reinterpret_cast<const half8*>(row + 8 * c);
+    auto slot_of = [&](const Slots64& v, int sidx) { return v.get(sidx); };
+    if (sel_out && live && lane < nw)
+      sel_out[(long)m * nw + lane] = (uint32_t)(slot_of(sel_sl, lane >> 1) >> (32 * (lane & 1)));
+    if constexpr (KEEPOUT) {
+      // one lane per 64-neuron K-step ORs in the neuron ranges of the (at most 64 / S + 2) experts it overlaps
+      for (int ks = lane; ks < (F >> 6); ks += 64) {
+        const int n0 = 64 * ks;
+        const int e0 = n0 / S, e1 = (n0 + 63) / S;
+        unsigned long long w = 0;
+        for (int e = e0; e <= e1 && e < E; ++e) {
+          if ((slot_of(keep_sl, e >> 6) >> (e & 63)) & 1ull) {
+            const int lo = max(e * S, n0) - n0, hi = min((e + 1) * S, n0 + 64) - n0;
+            w |= (hi - lo >= 64 ? ~0ull : ((1ull << (hi - lo)) - 1ull)) << lo;
+          }
+        }
+        kw_dyn[(wave * TPW + t) * kws + ks] = w;
+      }
+    } else {
+      if (!live) return;  // wave-uniform
+      half_t* row = P + (long)m * ldp;
+      for (int c = lane; c < (F >> 3); c += 64) {
+        unsigned kb = 0;  // keep bit per neuron of this 8-neuron chunk
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (!((kb >> j) & 1u)) v[j] = (half_t)0.f;
+        for (int j = 0; j < 8; ++j) {
+          const int e = (8 * c + j) / S;
+          kb |= (unsigned)((slot_of(keep_sl, e >> 6) >> (e & 63)) & 1ull) << j;
+        }
+        if (kb == 0xffu) continue;
+        half8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (kb) {
+          v = *reinterpret_cast<const half8*>(row + 8 * c);
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (!((kb >> j) & 1u)) v[j] = (half_t)0.f;
+        }
+        *reinterpret_cast<half8*>(row + 8 * c) = v;
+      }
     }
-    *reinterpret_cast<half8*>(row + 8 * c) = v;
+  };
+  process(sc0, 0);
+  process(sc1, 1);
+  process(sc2, 2);
+  process(sc3, 3);
+  if constexpr (KEEPOUT) {
+    __syncthreads();
+    const int m0 = blockIdx.x * TPB, nks = F >> 6;
+    for (int idx = threadIdx.x; idx < nks * TPB; idx += WPB * 64) {
+      const int ks = idx / TPB, t = idx - ks * TPB;
+      if (m0 + t < M) keep[(long)ks * M + m0 + t] = kw_dyn[t * kws + ks];
+    }
   }
 }
 
 }  // namespace
 
-extern "C" int sdmoe_moe_topk_mask(void* P, long ldp, int M, int F, int E, int esize, int k, const void* score,
-                                   long ld_score, const unsigned* removed_bits, unsigned* sel_out, void* stream) {
-  if (!P || !score || M < 0 || F <= 0 || E <= 0 || esize <= 0) return SDMOE_EARG;
-  if (M == 0) return SDMOE_OK;
-  if (F % 8 || ldp % 8 || E * esize != F || ld_score < E) return SDMOE_ESHAPE;
-  if (E > 256) return SDMOE_EUNSUP;
-  if (k < 0 || k > E) return SDMOE_EARG;
-  hipStream_t s = (hipStream_t)stream;
-  const int blocks = (M + 3) / 4;
-  half_t* Pp = (half_t*)P;
-  const half_t* sc = (const half_t*)score;
-  const uint32_t* rm = (const uint32_t*)removed_bits;
+template <bool KEEPOUT>
+int launch_topk(half_t* P, long ldp, int M, int F, int E, int esize, int k, const half_t* sc, long ld_score,
+                const uint32_t* rm, uint32_t* sel_out, unsigned long long* keep, hipStream_t s) {
+  const int blocks = (M + 15) / 16;  // 4 waves x 4 tokens per workgroup
+  const size_t lds = KEEPOUT ? (size_t)16 * ((F >> 6) + 1) * 8 : 0;
 #define SDMOE_TOPK_MASK(SL, SC) \
-  moe_topk_mask_kernel<SL, SC><<<blocks, 256, 0, s>>>(Pp, ldp, M, F, E, esize, k, sc, ld_score, rm, sel_out)
+  moe_topk_mask_kernel<SL, SC, KEEPOUT><<<blocks, 256, lds, s>>>(P, ldp, M, F, E, esize, k, sc, ld_score, rm, \
+                                                                   sel_out, keep)
   if (esize == 20) {  // the reference's expert size (KMeansConstrained, 20 neurons): divisions by a constant
     if (E <= 64) SDMOE_TOPK_MASK(1, 20);
     else if (E <= 128) SDMOE_TOPK_MASK(2, 20);
@@ -246,6 +304,28 @@ extern "C" int sdmoe_moe_topk_mask(void* P, long ldp, int M, int F, int E, int e
 #undef SDMOE_TOPK_MASK
   SDMOE_CHECK_LAUNCH();
   return SDMOE_OK;
+}
+
+extern "C" int sdmoe_moe_topk_mask(void* P, long ldp, int M, int F, int E, int esize, int k, const void* score,
+                                   long ld_score, const unsigned* removed_bits, unsigned* sel_out, void* stream) {
+  if (!P || !score || M < 0 || F <= 0 || E <= 0 || esize <= 0) return SDMOE_EARG;
+  if (M == 0) return SDMOE_OK;
+  if (F % 8 || ldp % 8 || E * esize != F || ld_score < E) return SDMOE_ESHAPE;
+  if (E > 256) return SDMOE_EUNSUP;
+  if (k < 0 || k > E) return SDMOE_EARG;
+  return launch_topk<false>((half_t*)P, ldp, M, F, E, esize, k, (const half_t*)score, ld_score,
+                            (const uint32_t*)removed_bits, sel_out, nullptr, (hipStream_t)stream);
+}
+
+extern "C" int sdmoe_moe_topk_keep(int M, int F, int E, int esize, int k, const void* score, long ld_score,
+                                   const unsigned* removed_bits, void* keep, unsigned* sel_out, void* stream) {
+  if (!keep || !score || M < 0 || F <= 0 || E <= 0 || esize <= 0) return SDMOE_EARG;
+  if (M == 0) return SDMOE_OK;
+  if (F % 64 || E * esize != F || ld_score < E) return SDMOE_ESHAPE;
+  if (E > 256 || esize > 40) return SDMOE_EUNSUP;
+  if (k < 0 || k > E) return SDMOE_EARG;
+  return launch_topk<true>(nullptr, 0, M, F, E, esize, k, (const half_t*)score, ld_score, (const uint32_t*)removed_bits,
+                           sel_out, (unsigned long long*)keep, (hipStream_t)stream);
 }
 
 extern "C" int sdmoe_geglu_route(const void* Y, long ldy, int M, int F, int E, int k, int act, const int* labels,

@@ -284,6 +284,41 @@ def moe_topk_mask(P, score, routing: "Routing", removed=None, sel_out=None):
     return P
 
 
+def moe_topk_keep(score, routing: "Routing", M: int, removed=None, sel_out=None, keep=None):
+    """Top-k selection of sdmoe_moe_topk_mask as keep bits for sdmoe_linear_keep: int64 [F/64, M] words, bit j of
+    word (s, m) = expert-major neuron 64 s + j of token m kept."""
+    lib = _lib.load()
+    sp, lds = _rows(score, "score")
+    F = routing.E * routing.esize
+    if keep is None:
+        keep = torch.empty((F // 64, M), dtype=torch.int64, device=score.device)
+    if tuple(keep.shape) != (F // 64, M) or keep.dtype != torch.int64:
+        raise ValueError(f"keep must be int64 [{F // 64}, {M}], got {keep.dtype} {tuple(keep.shape)}")
+    st = lib.sdmoe_moe_topk_keep(M, F, routing.E, routing.esize, routing.k, sp, lds, _ptr(removed),
+                                 _dev(keep, "keep", torch.int64), _ptr(sel_out), _stream())
+    _lib.check(st, "sdmoe_moe_topk_keep")
+    return keep
+
+
+def linear_keep(x, keep, w, bias=None, *, residual=None, out=None):
+    """out = (x with the neurons whose keep bit is clear zeroed) @ w.T + bias + residual (sdmoe_linear_keep)."""
+    lib = _lib.load()
+    xp, lda = _rows(x, "x")
+    M, K = x.shape
+    N = w.shape[0]
+    if w.shape[1] != K or tuple(keep.shape) != (K // 64, M) or keep.dtype != torch.int64:
+        raise ValueError(f"linear_keep: x {tuple(x.shape)}, keep {tuple(keep.shape)}, w {tuple(w.shape)} mismatch")
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float16, device=x.device)
+    op, ldc = _rows(out, "out")
+    rp, ldr = (None, 0) if residual is None else _rows(residual, "residual")
+    ws = _workspace(x.device)
+    st = lib.sdmoe_linear_keep(xp, lda, _dev(keep, "keep", torch.int64), _dev(w, "w"), w.stride(0), _ptr(bias), rp,
+                               ldr, op, ldc, M, N, K, ws.data_ptr(), ws.numel(), _stream())
+    _lib.check(st, "sdmoe_linear_keep")
+    return out
+
+
 def removed_bits(expert_ids, num_experts: int, device) -> torch.Tensor:
     """uint32-packed (as int32) bitmask of removed experts."""
     nw = (num_experts + 31) // 32

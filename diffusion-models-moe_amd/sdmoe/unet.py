@@ -26,6 +26,7 @@ from .config import UNetConfig
 
 CTX_LEN = 77
 FUSED_GEGLU = True  # fused projection+GEGLU(+expert scores) path where eligible (tests flip it for A/B parity)
+FUSED_KEEP = True   # fused path: top-k mask applied inside the down projection (sdmoe_linear_keep) instead of a pass
 IN_PAD = 64    # conv_in input channels padded 4 -> 64 (K-step of the implicit GEMM)
 OUT_PAD = 8    # conv_out output channels padded 4 -> 8 (16-B epilogue stores)
 
@@ -121,6 +122,7 @@ class GEGLU(nn.Module):
         # routed() call produced (its output pointer and permutation) for the FeedForward down projection
         self._allow_permuted_out = False
         self._out_perm = None
+        self._out_keep = None  # (keep bits, output pointer) when the top-k mask is left to the down projection
         self._il_key = None
         self._il = None
 
@@ -163,6 +165,7 @@ class GEGLU(nn.Module):
         routing = self.routing()
         act = act_code(self.gelu)
         self._out_perm = None
+        self._out_keep = None
         if (FUSED_GEGLU and self._allow_permuted_out and not want_gate and self.inner_dim % 80 == 0 and x2.shape[1] % 64 == 0
                 and (routing is None or routing.fusable)):
             w_il, b_il = self._interleaved(routing)
@@ -171,7 +174,13 @@ class GEGLU(nn.Module):
             else:
                 score = torch.empty((x2.shape[0], routing.E), dtype=torch.float16, device=x.device)
                 out = ops.linear_geglu(x2, w_il, b_il, act, score=score, esize=routing.esize)
-                ops.moe_topk_mask(out, score, routing, removed=removed, sel_out=sel_out)
+                if FUSED_KEEP and routing.F % 64 == 0:
+                    # the dropped experts' neurons are zeroed by the down projection as it reads them
+                    # (sdmoe_linear_keep); `out` is then the unmasked product, an operand only FeedForward consumes
+                    keep = ops.moe_topk_keep(score, routing, x2.shape[0], removed=removed, sel_out=sel_out)
+                    self._out_keep = (keep, out.data_ptr())
+                else:
+                    ops.moe_topk_mask(out, score, routing, removed=removed, sel_out=sel_out)
                 self._out_perm = (routing, out.data_ptr())
             return out.view(*shp[:-1], self.inner_dim), None
         y = self.proj.run(x2)
@@ -248,7 +257,11 @@ class FeedForward(nn.Module):
         h2 = h.reshape(-1, h.shape[-1])
         perm = geglu._out_perm
         if perm is not None and perm[1] == h2.data_ptr():
-            return ops.linear(h2, self._down_weight_permuted(perm[0]), down.bias, residual=residual)
+            wp = self._down_weight_permuted(perm[0])
+            keep = geglu._out_keep
+            if keep is not None and keep[1] == h2.data_ptr():
+                return ops.linear_keep(h2, keep[0], wp, down.bias, residual=residual)
+            return ops.linear(h2, wp, down.bias, residual=residual)
         return down.run(h2, residual=residual)
 
 

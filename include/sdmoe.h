@@ -123,6 +123,23 @@ int sdmoe_moe_topk_mask(void* P, long ldp, int M, int F, int E, int esize, int k
                         long ld_score, const unsigned* removed_bits, unsigned* sel_out, void* stream);
 
 /*
+ * The same routing with the mask moved into the FFN down projection (ff.net.2) instead of a pass over P:
+ *  sdmoe_moe_topk_keep: the selection of sdmoe_moe_topk_mask (removed experts score 0, top-k, ties toward the
+ *    lowest id) written as keep bits of the expert-major permuted neurons: keep [F/64][M] 64-bit words, bit j of
+ *    word (s, m) = neuron 64 s + j of token m is kept (selected and not removed). P is not touched. F % 64 == 0.
+ *  sdmoe_linear_keep: C = (A with every dropped neuron zeroed) @ W^T + bias + R, the zeroing applied to the A
+ *    fragments after their LDS read, so the result is bit-identical to sdmoe_moe_topk_mask followed by
+ *    sdmoe_linear. A [M, K] (K = F), keep as above, W [N, K]. K % 64 == 0.
+ * Replaces: gate[cur_mask == 0] = 0 and hidden_states * gate of MOEFy / RemoveExperts.hook_fn (moefy.py:23-26,
+ * remove_skilled_experts.py:49-55) feeding ff.net.2 (diffusers FeedForward), without a pass over the product.
+ */
+int sdmoe_moe_topk_keep(int M, int F, int E, int esize, int k, const void* score, long ld_score,
+                        const unsigned* removed_bits, void* keep, unsigned* sel_out, void* stream);
+int sdmoe_linear_keep(const void* A, long lda, const void* keep, const void* W, long ldw, const void* bias,
+                      const void* R, long ldr, void* C, long ldc, int M, int N, int K, float* workspace,
+                      long workspace_floats, void* stream);
+
+/*
  * Skill discovery on the same hook seam.
  * sdmoe_expert_mean_topk — GetExperts.hook_fn (neuron_receivers/get_experts.py:50-83): mean over tokens of the
  *   fp16 expert scores [M, E] (score_within_bb.mean(0): fp32 accumulate, one rounding to fp16), restricted to the

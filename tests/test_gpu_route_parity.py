@@ -198,6 +198,41 @@ def test_fused_geglu_bit_exact_vs_unfused(M, C, E, k, act, nrem):
     assert torch.equal(out, out_u)
 
 
+@pytest.mark.parametrize("M,C,E,k,nrem,N", [(4096, 320, 64, 12, 5, 320), (1000, 320, 64, 12, 0, 320),
+                                            (2048, 640, 128, 25, 9, 640), (777, 1280, 256, 51, 20, 1280),
+                                            (256, 1280, 256, 51, 0, 1280), (333, 640, 128, 128, 0, 640)])
+def test_keep_mask_in_down_projection_bit_exact(M, C, E, k, nrem, N):
+    """sdmoe_moe_topk_keep + sdmoe_linear_keep (the mask applied to the down projection's A fragments) vs
+    sdmoe_moe_topk_mask + sdmoe_linear: same top-k bits, keep bits = the zero pattern of the masked product, and a
+    bit-identical down projection (+bias +residual), across tile choices, M tails and split-K (M = 256, K = 5120)."""
+    g = torch.Generator().manual_seed(3 * M + C)
+    F = 4 * C
+    x = torch.randn(M, C, generator=g).half().to(DEV)
+    w = (torch.randn(2 * F, C, generator=g) * C ** -0.5).half().to(DEV)
+    b = (torch.randn(2 * F, generator=g) * 0.3).half().to(DEV)
+    wd = (torch.randn(N, F, generator=g) * F ** -0.5).half().to(DEV)
+    bd = (torch.randn(N, generator=g) * 0.1).half().to(DEV)
+    res = torch.randn(M, N, generator=g).half().to(DEV)
+    routing = ops.Routing(torch.randperm(F, generator=g) % E, E, k, DEV)
+    removed = ops.removed_bits(torch.randperm(E, generator=g)[:nrem].tolist(), E, DEV) if nrem else None
+    w_il, b_il = ops.interleave_geglu(w, b, routing.perm)
+    score = torch.empty((M, E), dtype=torch.float16, device=DEV)
+    P = ops.linear_geglu(x, w_il, b_il, ops.ACT_RELU, score=score, esize=routing.esize)
+    Pm = P.clone()
+    sel_m = torch.zeros((M, (E + 31) // 32), dtype=torch.int32, device=DEV)
+    sel_k = torch.zeros_like(sel_m)
+    ops.moe_topk_mask(Pm, score, routing, removed=removed, sel_out=sel_m)
+    keep = ops.moe_topk_keep(score, routing, M, removed=removed, sel_out=sel_k)
+    assert torch.equal(sel_m, sel_k)
+    kb = keep.cpu().numpy().view(np.uint64)  # [F/64, M]
+    bits = ((kb[:, :, None] >> np.arange(64, dtype=np.uint64)) & np.uint64(1)).astype(bool)  # [F/64, M, 64]
+    kmask = torch.from_numpy(np.ascontiguousarray(bits.transpose(1, 0, 2).reshape(M, F))).to(DEV)
+    assert torch.equal(Pm, torch.where(kmask, P, torch.zeros_like(P)))
+    y_ref = ops.linear(Pm, wd, bd, residual=res)
+    y = ops.linear_keep(P, keep, wd, bd, residual=res)
+    assert torch.equal(y, y_ref)
+
+
 def test_fused_geglu_dense_matches_unfused():
     M, C = 1500, 320
     g = torch.Generator().manual_seed(7)

@@ -346,6 +346,45 @@ def test_pipeline_fused_geglu_sd14(receiver):
     assert ffs and all(f._wperm is not None for f in ffs)  # the fused path actually ran
 
 
+def test_pipeline_keep_mask_bit_identical_sd14():
+    """Fused path with the top-k mask applied inside the down projection (sdmoe_linear_keep) vs the mask pass over
+    the product (sdmoe_moe_topk_mask): the down projection sees identical operands, so a U-Net evaluation and a
+    2-step RemoveExperts pipeline (top-k 0.2, removals active) are bit-identical."""
+    from moefication.helper import moefy_synthetic
+    from neuron_receivers import RemoveExperts
+    import sdmoe.unet as U
+    cfg = UNetConfig.sd14(16)
+    unet = UNet2DConditionModel.from_state_dict(make_state_dict(cfg, 5), cfg, DEV)
+    pipe = StableDiffusionPipeline(unet, DEV, num_inference_steps=2)
+    moefy_synthetic(pipe, 0.2, 20, seed=3)
+    lists = {t: {l: list(range(l % 5, 64, 7)) for l in range(16)} for t in range(51)}
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(2, 4, 16, 16, generator=g).to(DEV)
+    ctx = ctx_for(cfg, ["Starry night by Van Gogh"]).to(DEV)
+    geglus = [m for n, m in unet.named_modules() if n.endswith("ff.net.0")]
+    evals, outs, ran = [], [], []
+    for keep in (True, False):
+        U.FUSED_KEEP = keep
+        try:
+            rec = RemoveExperts(0, None, T=51, n_layers=16, store_gates=False, expert_indices=lists)
+            rec.prepare(pipe)
+            hooks = rec.register_hooks(pipe)
+            try:
+                evals.append(unet(x, 741.0, ctx))
+            finally:
+                rec.remove_hooks(hooks)
+            ran.append(all(m._out_keep is not None for m in geglus))
+            out, _ = RemoveExperts(0, None, T=51, n_layers=16, store_gates=False,
+                                   expert_indices=lists).observe_activation(pipe, ["a cat", "Starry night"])
+        finally:
+            U.FUSED_KEEP = True
+        outs.append(torch.stack(out))
+    assert ran == [True, False]
+    assert torch.isfinite(outs[0]).all()
+    assert torch.equal(evals[0], evals[1])
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_pipeline_pndm_remove_experts_tiny(tiny):
     """The reference's default scheduler: PNDM (skip_prk_steps) = num_inference_steps + 1 U-Net calls, the
     receiver's (t, l) counter advancing once per call (T = 6 for 5 steps, as T = 51 for 50). RemoveExperts with

@@ -87,8 +87,17 @@ def main():
         ms = timeit(lambda: ops.linear_geglu(x, w_il, b_il, ops.ACT_RELU, score=score, esize=routing.esize, out=out),
                     a.iters)
         rows.append((f"geglu-gemm M={M} F={F} K={C}", ms, 2.0 * M * 2 * F * C / ms / 1e9))
+        score.copy_(torch.randn(M, E, device=dev).half())
         ms = timeit(lambda: ops.moe_topk_mask(out, score, routing), a.iters)
         rows.append((f"topk-mask M={M} F={F} (GB/s)", ms, (M * F * 2 * 0.8 + M * E * 2) / ms / 1e6))
+        keep = ops.moe_topk_keep(score, routing, M)
+        ms = timeit(lambda: ops.moe_topk_keep(score, routing, M, keep=keep), a.iters)
+        rows.append((f"topk-keep M={M} E={E} (GB/s)", ms, (M * E * 2 + M * F / 8) / ms / 1e6))
+        wd = (torch.randn(C, F, device=dev) * F ** -0.5).half()
+        ms = timeit(lambda: ops.linear(out, wd), a.iters)
+        rows.append((f"down M={M} N={C} K={F}", ms, 2.0 * M * C * F / ms / 1e9))
+        ms = timeit(lambda: ops.linear_keep(out, keep, wd), a.iters)
+        rows.append((f"down-keep M={M} N={C} K={F}", ms, 2.0 * M * C * F / ms / 1e9))
         y = torch.empty(M, 2 * F, device=dev).half()
         ms = timeit(lambda: ops.linear(x, w, b, out=y), a.iters)
         rows.append((f"  unfused proj M={M} N={2 * F} K={C}", ms, 2.0 * M * 2 * F * C / ms / 1e9))
