@@ -259,3 +259,41 @@ extern "C" int sdmoe_wanda_mask(const void* W, long ldw, int C, int F, const voi
   SDMOE_CHECK_LAUNCH();
   return SDMOE_OK;
 }
+
+// ---- static "union-timesteps" mask (benchmarks/save_union_over_time.py:189-207) ----------------------------------
+// out bit = (number of the T per-timestep masks with the bit set) > threshold (select_ratio * timesteps), over T
+// bit-packed masks [T][nbytes] (t-th mask at bits + t * t_stride). One thread per 32-bit word: 32 counters in
+// registers, one coalesced 4-B load per mask.
+namespace {
+__global__ __launch_bounds__(256) void union_over_time_kernel(const uint32_t* __restrict__ bits, long t_stride_words,
+                                                              int T, long nwords, float thr,
+                                                              uint32_t* __restrict__ out) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < nwords; i += (long)gridDim.x * 256) {
+    unsigned cnt[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) cnt[j] = 0;
+    for (int t = 0; t < T; ++t) {
+      const uint32_t w = bits[(long)t * t_stride_words + i];
+#pragma unroll
+      for (int j = 0; j < 32; ++j) cnt[j] += (w >> j) & 1u;
+    }
+    uint32_t o = 0;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) o |= ((float)cnt[j] > thr ? 1u : 0u) << j;
+    out[i] = o;
+  }
+}
+}  // namespace
+
+extern "C" int sdmoe_union_over_time(const void* bits, long t_stride_bytes, int T, long nbytes, float threshold,
+                                     void* out, void* stream) {
+  if (!bits || !out || T <= 0 || nbytes <= 0) return SDMOE_EARG;
+  if (nbytes % 4 || t_stride_bytes % 4 || t_stride_bytes < nbytes) return SDMOE_ESHAPE;
+  const long nw = nbytes / 4;
+  long g = (nw + 255) / 256;
+  if (g > 4096) g = 4096;
+  union_over_time_kernel<<<(int)g, 256, 0, (hipStream_t)stream>>>((const uint32_t*)bits, t_stride_bytes / 4, T, nw,
+                                                                   threshold, (uint32_t*)out);
+  SDMOE_CHECK_LAUNCH();
+  return SDMOE_OK;
+}

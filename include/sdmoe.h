@@ -176,6 +176,16 @@ int sdmoe_sqdist_f32(const float* X, long ldx, const float* C, long ldc, int n, 
                      void* stream);
 int sdmoe_balanced_assign(const double* cost, int n, int k, double scale, int64_t* prices, int warm, int* labels);
 
+/*
+ * Static "union-timesteps" mask (benchmarks/save_union_over_time.py:189-207): out bit =
+ * (number of the T per-timestep Wanda masks with that bit set) > threshold, threshold = select_ratio * timesteps.
+ * bits: T bit-packed masks of nbytes each (mask t at bits + t * t_stride_bytes, the [C, F/8] layout of
+ * sdmoe_mask_weight); out: nbytes. Baking the result into ff.net.2 (W * (1 - M), :214-221) is sdmoe_mask_weight
+ * with Wm = W. nbytes % 4 == 0.
+ */
+int sdmoe_union_over_time(const void* bits, long t_stride_bytes, int T, long nbytes, float threshold, void* out,
+                          void* stream);
+
 /* diffusers get_timestep_embedding for one timestep (t_dev if non-NULL, else t), fp16 [dim]. */
 int sdmoe_timestep_embedding(void* out, const float* t_dev, float t, int dim, int flip_sin_to_cos, float freq_shift,
                              void* stream);

@@ -320,3 +320,23 @@ def test_oracle_constrained_kmeans_properties():
     for c in range(8):
         assert len(set(blob[lab == c].tolist())) == 1
     assert inertia < 80 * 16 * 0.1 ** 2 * 2
+
+
+def test_union_over_time_oracle_and_layer_order():
+    """Oracle of save_union_over_time.py:189-204 (strict > select_ratio * timesteps on the summed masks) and the
+    sorted ff.net.2 layer order it indexes masks by (:163-169) = the hook-call order of the U-Net."""
+    from oracle import hooks_ref as H
+    from sdmoe import union_bake
+    from sdmoe.config import UNetConfig
+    from sdmoe.unet import UNet2DConditionModel
+    from sdmoe.weights import make_state_dict
+    m = [np.array([[1, 0, 1, 1]]), np.array([[1, 0, 0, 1]]), np.array([[1, 1, 0, 1]]), np.array([[0, 0, 0, 1]])]
+    assert H.union_over_time(m, 0.5, 4).tolist() == [[1, 0, 0, 1]]   # counts 3,1,1,4 > 2
+    assert H.union_over_time(m, 0.75, 4).tolist() == [[0, 0, 0, 1]]  # > 3
+    assert H.union_over_time(m, 0.0, 4).tolist() == [[1, 1, 1, 1]]
+    cfg = UNetConfig.sd14(8)
+    unet = UNet2DConditionModel.from_state_dict(make_state_dict(cfg, 0), cfg, "cpu")
+    names = [n for n, _ in union_bake.down_projection_layers(unet)]
+    hooked = [n for n, _ in unet.named_modules() if n.endswith("ff.net.2")]
+    assert len(names) == 16 and names == hooked
+    assert [tuple(m.weight.shape) for _, m in union_bake.down_projection_layers(unet)][:2] == [(320, 1280)] * 2
