@@ -49,6 +49,8 @@ def parse():
     p.add_argument("--topk-mask", choices=["down", "pass"], default="down",
                    help="down: the top-k mask is applied by the down projection as it reads the GEGLU product "
                         "(sdmoe_linear_keep); pass: a separate masking pass over the product (A/B reference)")
+    p.add_argument("--decode", action="store_true",
+                   help="also run the VAE decoder inside the timed step (end-to-end images; the metric excludes it)")
     p.add_argument("--no-roofline", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-evals", type=int, default=2, help="CPU oracle U-Net evaluations to time")
@@ -91,6 +93,10 @@ def build(args, world, rank, dev):
     cfg = UNetConfig.sdxl(128) if args.model == "sdxl" else UNetConfig.sd14(64)
     pipe = StableDiffusionPipeline.synthetic(cfg, seed=0, device=dev, num_inference_steps=args.inference_steps,
                                              scheduler=args.scheduler)
+    if args.decode:
+        from sdmoe.vae import AutoencoderKLDecoder, VAEConfig, make_vae_state_dict
+        pipe.vae = AutoencoderKLDecoder(make_vae_state_dict(VAEConfig.sd14(), 0), VAEConfig.sd14(), dev)
+        pipe.output_type = "pt"
     find_and_change_geglu(pipe.unet)                  # relufied U-Net (config 2/3)
     moefy_synthetic(pipe, args.topk, 20, seed=0)      # E = 4C/20 experts, k = int(E*topk)
     geglus = [m for n, m in pipe.unet.named_modules() if n.endswith("ff.net.0")]
@@ -304,7 +310,8 @@ def main():
                                    f"{'RemoveExperts skilled-expert mask' if args.mask != 'none' else 'no mask'}"
                                    f"{' + union Wanda mask' if args.mask == 'union' else ''}, "
                                    f"{8 * cfg.sample_size}^2 (4x{cfg.sample_size}x{cfg.sample_size} latents), "
-                                   f"{args.inference_steps} {args.scheduler.upper()} steps, CFG 7.5",
+                                   f"{args.inference_steps} {args.scheduler.upper()} steps, CFG 7.5"
+                                   f"{' + VAE decode to 512^2 RGB' if args.decode else ''}",
                        "prompts_per_gpu": args.batch, "global_batch": world * args.batch,
                        "parallelism": f"dp{world}"},
             "step_mfma_frac": round(value / world * TFLOP_PER_IMAGE[args.model] / PEAK_FP16_TFLOPS, 4),

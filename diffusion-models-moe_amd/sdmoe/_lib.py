@@ -39,6 +39,8 @@ SIGNATURES = {
     "sdmoe_colnorm_accum": [_P, _L, _I, _I, _P, _P, _L, _P],
     "sdmoe_wanda_mask": [_P, _L, _I, _I, _P, _P, _I, _P, _P],
     "sdmoe_union_over_time": [_P, _L, _I, _L, _F, _P, _P],
+    "sdmoe_softmax_rows": [_P, _L, _P, _L, _I, _I, _P],
+    "sdmoe_transpose": [_P, _L, _P, _L, _I, _I, _P],
     "sdmoe_timestep_embedding_rows": [_P, _L, _P, _I, _I, _I, _I, _F, _P],
     "sdmoe_prepare_input": [_P, _P, _I, _I, _L, _I, _P],
     "sdmoe_cfg_ddim_step": [_P, _L, _P, _I, _I, _I, _F, _F, _F, _P, _L, _P],

@@ -468,6 +468,30 @@ def cfg_multistep_step(eps: torch.Tensor, lat: torch.Tensor, do_cfg: bool, guida
     return lat
 
 
+def softmax_rows(x, out=None):
+    """Row softmax of a 2-D fp16 view (fp32 max / sum), sdmoe_softmax_rows."""
+    lib = _lib.load()
+    xp, ldx = _rows(x, "x")
+    R, N = x.shape
+    if out is None:
+        out = torch.empty((R, N), dtype=torch.float16, device=x.device)
+    op, ldy = _rows(out, "out")
+    _lib.check(lib.sdmoe_softmax_rows(xp, ldx, op, ldy, R, N, _stream()), "sdmoe_softmax_rows")
+    return out
+
+
+def transpose(x, out=None):
+    """[R, C] fp16 view -> contiguous [C, R] (sdmoe_transpose)."""
+    lib = _lib.load()
+    xp, ldx = _rows(x, "x")
+    R, C = x.shape
+    if out is None:
+        out = torch.empty((C, R), dtype=torch.float16, device=x.device)
+    op, ldy = _rows(out, "out")
+    _lib.check(lib.sdmoe_transpose(xp, ldx, op, ldy, R, C, _stream()), "sdmoe_transpose")
+    return out
+
+
 def add(a, b, out=None):
     lib = _lib.load()
     if out is None:

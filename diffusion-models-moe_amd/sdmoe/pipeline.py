@@ -103,7 +103,8 @@ def sdxl_time_ids(height: int, width: int) -> list:
 def initial_latents(seed: int, index: int, cfg: UNetConfig) -> torch.Tensor:
     """Per-prompt latents from a CPU generator seeded by (seed, global prompt index): identical for any
     world size / sharding."""
-    g = torch.Generator().manual_seed(int(seed) * 1_000_003 + int(index))
+    # masked to 63 bits: torch.initial_seed() of an unseeded process is a random 64-bit value
+    g = torch.Generator().manual_seed((int(seed) * 1_000_003 + int(index)) & 0x7FFF_FFFF_FFFF_FFFF)
     return torch.randn((1, cfg.in_channels, cfg.sample_size, cfg.sample_size), generator=g)
 
 
@@ -114,7 +115,7 @@ class PipelineOutput:
 
 class StableDiffusionPipeline:
     def __init__(self, unet: UNet2DConditionModel, device="cuda", num_inference_steps=50, guidance_scale=7.5,
-                 scheduler="ddim"):
+                 scheduler="ddim", vae=None):
         if scheduler not in ("ddim", "pndm"):
             raise ValueError(f"scheduler must be 'ddim' or 'pndm', got {scheduler!r}")
         self.scheduler = scheduler  # "pndm": the reference's default (51 U-Net calls per 50 steps)
@@ -124,6 +125,8 @@ class StableDiffusionPipeline:
         self.num_inference_steps = num_inference_steps
         self.guidance_scale = guidance_scale
         self.prompt_offset = 0  # global index of the first prompt (data-parallel shards set this per rank)
+        self.vae = vae  # sdmoe.vae.AutoencoderKLDecoder or None (output_type "pt"/"np" then decodes the latents)
+        self.output_type = "latent"  # default of __call__'s output_type (the receivers call pipe(prompt) bare)
 
     @classmethod
     def synthetic(cls, cfg: UNetConfig | None = None, seed: int = 0, device="cuda", **kw):
@@ -154,7 +157,7 @@ class StableDiffusionPipeline:
         return {"text_embeds": pooled, "time_ids": tids}
 
     def __call__(self, prompt, num_inference_steps=None, guidance_scale=None, latents=None, seed=None,
-                 prompt_offset=None, safety_checker=None, output_type="latent", **unused):
+                 prompt_offset=None, safety_checker=None, output_type=None, **unused):
         prompts = [prompt] if isinstance(prompt, str) else list(prompt)
         B = len(prompts)
         cfg = self.config
@@ -188,12 +191,26 @@ class StableDiffusionPipeline:
             for t, coef, flags in pndm_schedule(steps):
                 self.unet.forward_nhwc(x_in, float(t), ctx, out=eps, add_hidden=add_hidden)
                 ops.cfg_multistep_step(eps, lat, do_cfg, g, hist, cur, coef, flags, next_in=x_in)
-            return PipelineOutput(images=[lat[i] for i in range(B)])
-        ts, a_t, a_prev = ddim_schedule(steps)
-        for s, t in enumerate(ts):
-            self.unet.forward_nhwc(x_in, float(t), ctx, out=eps, add_hidden=add_hidden)
-            ops.cfg_ddim_step(eps, lat, do_cfg, g, a_t[s], a_prev[s], next_in=x_in)
-        return PipelineOutput(images=[lat[i] for i in range(B)])
+        else:
+            ts, a_t, a_prev = ddim_schedule(steps)
+            for s, t in enumerate(ts):
+                self.unet.forward_nhwc(x_in, float(t), ctx, out=eps, add_hidden=add_hidden)
+                ops.cfg_ddim_step(eps, lat, do_cfg, g, a_t[s], a_prev[s], next_in=x_in)
+        return PipelineOutput(images=self._finish(lat, output_type or self.output_type))
+
+    def _finish(self, lat, output_type):
+        """output_type "latent": the denoised latents; "pt" / "np": vae.decode(latents / scaling_factor) then
+        (x / 2 + 0.5).clamp(0, 1) as diffusers' VaeImageProcessor does (images [3, H, W] / [H, W, 3])."""
+        B = lat.shape[0]
+        if output_type == "latent":
+            return [lat[i] for i in range(B)]
+        if self.vae is None:
+            raise ValueError(f"output_type {output_type!r} needs a VAE decoder (pipe.vae = AutoencoderKLDecoder(...))")
+        from .vae import postprocess
+        img = postprocess(self.vae.decode(lat))
+        if output_type == "np":
+            return [img[i].permute(1, 2, 0).cpu().numpy() for i in range(B)]
+        return [img[i] for i in range(B)]
 
     def to(self, device):
         """Weights are placed at construction; kept for the reference's `model.to(args.gpu)` call shape."""

@@ -186,6 +186,16 @@ int sdmoe_balanced_assign(const double* cost, int n, int k, double scale, int64_
 int sdmoe_union_over_time(const void* bits, long t_stride_bytes, int T, long nbytes, float threshold, void* out,
                           void* stream);
 
+/*
+ * VAE decoder helpers (diffusers AutoencoderKL.decode, external): the decoder mid-block's
+ * single 512-wide attention head runs as sdmoe_linear (S = Q K^T) -> sdmoe_softmax_rows -> sdmoe_linear (O = P V,
+ * with V^T from sdmoe_transpose).
+ * sdmoe_softmax_rows — Y[r, :] = softmax(X[r, :]) for R rows of N (fp16, fp32 math; N % 8 == 0, N <= 8192).
+ * sdmoe_transpose — Y [C, R] = X [R, C]^T, fp16, any leading dimensions.
+ */
+int sdmoe_softmax_rows(const void* X, long ldx, void* Y, long ldy, int R, int N, void* stream);
+int sdmoe_transpose(const void* X, long ldx, void* Y, long ldy, int R, int C, void* stream);
+
 /* diffusers get_timestep_embedding for one timestep (t_dev if non-NULL, else t), fp16 [dim]. */
 int sdmoe_timestep_embedding(void* out, const float* t_dev, float t, int dim, int flip_sin_to_cos, float freq_shift,
                              void* stream);

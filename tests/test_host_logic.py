@@ -340,3 +340,31 @@ def test_union_over_time_oracle_and_layer_order():
     hooked = [n for n, _ in unet.named_modules() if n.endswith("ff.net.2")]
     assert len(names) == 16 and names == hooked
     assert [tuple(m.weight.shape) for _, m in union_bake.down_projection_layers(unet)][:2] == [(320, 1280)] * 2
+
+
+def test_vae_decoder_architecture():
+    """SD-1.x AutoencoderKL decoder layout (diffusers naming): mid block (2 ResNets + one attention), 4 up blocks of
+    3 ResNets, shortcuts where the width changes (512->256, 256->128), 3 upsamplers, conv_out to RGB."""
+    from sdmoe.vae import VAEConfig, vae_param_specs
+    specs = {n: s for n, s, _ in vae_param_specs(VAEConfig.sd14())}
+    assert specs["decoder.conv_in.weight"] == (512, 4, 3, 3)
+    assert specs["decoder.mid_block.attentions.0.to_q.weight"] == (512, 512)
+    assert sum(n.endswith("conv1.weight") for n in specs) == 2 + 4 * 3
+    assert sorted(n for n in specs if "conv_shortcut.weight" in n) == [
+        "decoder.up_blocks.2.resnets.0.conv_shortcut.weight", "decoder.up_blocks.3.resnets.0.conv_shortcut.weight"]
+    assert sum("upsamplers" in n and n.endswith("weight") for n in specs) == 3
+    assert specs["decoder.conv_out.weight"] == (3, 128, 3, 3)
+    n = sum(int(torch.tensor(s).prod()) for s in specs.values())
+    assert 49_000_000 < n < 50_000_000  # ~49.5M decoder parameters
+
+
+def test_initial_latents_unseeded_process_seed():
+    """An unseeded process's torch.initial_seed() is a random 64-bit value; the per-prompt latent seed must not
+    overflow the generator (seeds below 2^63 / 1000003 keep their old streams)."""
+    from sdmoe.config import UNetConfig
+    from sdmoe.pipeline import initial_latents
+    cfg = UNetConfig.tiny(8)
+    a = initial_latents(2 ** 64 - 1, 3, cfg)
+    assert a.shape == (1, 4, 8, 8) and torch.isfinite(a).all()
+    g = torch.Generator().manual_seed(7 * 1_000_003 + 2)
+    assert torch.equal(initial_latents(7, 2, cfg), torch.randn((1, 4, 8, 8), generator=g))
