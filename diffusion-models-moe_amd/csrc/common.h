@@ -50,12 +50,13 @@ SDMOE_DEV float wave_max(float v) {
 }
 
 // Activation kinds shared by the host ABI (include/sdmoe.h).
-enum { ACT_NONE = 0, ACT_SILU = 1, ACT_GELU = 2, ACT_RELU = 3 };
+enum { ACT_NONE = 0, ACT_SILU = 1, ACT_GELU = 2, ACT_RELU = 3, ACT_QUICK_GELU = 4 };
 
 SDMOE_DEV float apply_act(float v, int act) {
   if (act == ACT_SILU) return silu_f(v);
   if (act == ACT_GELU) return gelu_erf_f(v);
   if (act == ACT_RELU) return v > 0.f ? v : 0.f;
+  if (act == ACT_QUICK_GELU) return v / (1.0f + __expf(-1.702f * v));  // CLIP quick_gelu: x*sigmoid(1.702x)
   return v;
 }
 

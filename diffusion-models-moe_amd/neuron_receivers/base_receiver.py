@@ -15,6 +15,15 @@ import torch
 from sdmoe.unet import GEGLU, LoRACompatibleLinear  # noqa: F401  (re-exported for `replace_fn=GEGLU`)
 
 
+def text_mlp_modules(model):
+    """CLIPMLP modules of model.text_encoder with 'mlp' and 'encoder.layers' in the name (base_receiver.py:62-63)."""
+    from sdmoe.clip import CLIPMLP
+    te = getattr(model, "text_encoder", None)
+    if te is None:
+        raise ValueError("hook_module='text' needs a pipeline with a text_encoder (sdmoe.clip.CLIPTextModel)")
+    return [(n, m) for n, m in te.named_modules() if isinstance(m, CLIPMLP) and 'mlp' in n and 'encoder.layers' in n]
+
+
 class GELU(torch.nn.Module):
     """Placeholder for diffusers' GELU projection class (PixArt path, out of scope)."""
 
@@ -39,7 +48,7 @@ class BaseNeuronReceiver:
         raise NotImplementedError
 
     def text_hook_fn(self, module, input, output):
-        raise NotImplementedError("text-encoder hooks are outside this tier (SURVEY §2 #5)")
+        raise NotImplementedError(f"{type(self).__name__} has no text-encoder hook body")
 
     def remove_hooks(self, hooks):
         for hook in hooks:
@@ -56,13 +65,18 @@ class BaseNeuronReceiver:
         return h
 
     def hook_modules(self, model):
-        """(name, module) pairs this receiver hooks: replace_fn instances with 'ff.net' in the name."""
+        """(name, module) pairs this receiver hooks: replace_fn instances with 'ff.net' in the name (unet,
+        :46-57), or the text encoder's CLIPMLP modules under 'encoder.layers' (hook_module='text', :59-65)."""
+        if self.hook_module == 'text':
+            return text_mlp_modules(model)
         if self.hook_module != 'unet':
-            raise NotImplementedError("only hook_module='unet' is on the hot path")
+            raise ValueError(f"hook_module must be 'unet' or 'text', got {self.hook_module!r}")
         return [(n, m) for n, m in model.unet.named_modules() if isinstance(m, self.replace_fn) and 'ff.net' in n]
 
     def register_hooks(self, model, bboxes=None):
         hooks = []
+        if self.hook_module == 'text':
+            return [self._register(m, self.text_hook_fn) for _, m in self.hook_modules(model)]
         for name, module in self.hook_modules(model):
             hooks.append(self._register(module, self.hook_fn))
             module.bounding_box = bboxes[name + '.proj.weight'] if bboxes is not None else None

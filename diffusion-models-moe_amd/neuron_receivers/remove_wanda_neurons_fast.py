@@ -7,7 +7,8 @@ remove_timesteps is stored but, as in the reference's Fast receiver, not consult
 MI355X layout: masks are bit-packed [C, 4C/8] and uploaded once (all (t, l): 316 MB for SD-1.4 at T=51, vs
 ~20 GB as dense int64 in the reference); the GEMM zeroes masked weights while staging W tiles, so there is no
 per-call host->device mask copy, no W.clone() and no second GEMM (reference K9).
-The GEGLU variant hook_fn (:31-61, mask over the gate half of proj.weight) uses the same bitmask path.
+The GEGLU variant hook_fn (:31-61, mask over the gate half of proj.weight) uses the same bitmask path, and so does
+the text-encoder variant text_hook_fn (:85-101, hook_module='text': mask M[0][l] over CLIPMLP.fc2).
 """
 from __future__ import annotations
 
@@ -68,21 +69,22 @@ class WandaRemoveNeuronsFast(NeuronPredictivity):
         return d
 
     def hook_modules(self, model):
-        if self.hook_module != 'unet':
-            raise NotImplementedError("text-encoder hooks are outside this tier")
+        if self.hook_module == 'text':
+            return super().hook_modules(model)  # CLIPMLP modules (:114-120)
         # remove_wanda_neurons_fast.py:107-112: LoRACompatibleLinear, 'ff.net' in name, not a '.proj'
         return [(n, m) for n, m in model.unet.named_modules()
                 if isinstance(m, LoRACompatibleLinear) and 'ff.net' in n and 'proj' not in n]
 
     def prepare(self, model):
         mods = [m for _, m in self.hook_modules(model)]
-        dev = mods[0].weight.device
+        dev = (mods[0].fc2 if self.hook_module == 'text' else mods[0]).weight.device
         for t in range(self.T):
             for l in range(self.n_layers):
                 self.device_bits(t, l, dev)
 
     def register_hooks(self, model, bboxes=None):
-        return [self._register(m, self.linear_hook_fn) for _, m in self.hook_modules(model)]
+        fn = self.text_hook_fn if self.hook_module == 'text' else self.linear_hook_fn
+        return [self._register(m, fn) for _, m in self.hook_modules(model)]
 
     def observe_activation(self, model, ann, bboxes=None):
         self.prepare(model)
@@ -97,6 +99,19 @@ class WandaRemoveNeuronsFast(NeuronPredictivity):
         y = module.run(x.reshape(-1, x.shape[-1]), wmask_bits=bits)
         self.update_time_layer()
         return y.view(*x.shape[:-1], module.weight.shape[0])
+
+    def text_hook_fn(self, module, input, output):
+        """remove_wanda_neurons_fast.py:85-101: CLIPMLP with fc2.weight * (1 - M[0][layer]) — always timestep 0
+        (text masks have T = 1); fc1 + act in one GEMM epilogue, the mask applied while fc2's W tiles stage."""
+        x = input[0]
+        fc2 = module.fc2
+        bits = self.device_bits(0, self.layer, fc2.weight.device)
+        if bits.shape[0] != fc2.weight.shape[0] or bits.shape[1] * 8 != fc2.weight.shape[1]:
+            raise ValueError(f"text mask (0,{self.layer}) shape {tuple(bits.shape)} does not match fc2 weight "
+                             f"{tuple(fc2.weight.shape)}")
+        y = module.run(x.reshape(-1, x.shape[-1]), wmask_bits=bits)
+        self.update_time_layer()
+        return y.view(*x.shape[:-1], fc2.weight.shape[0])
 
     def hook_fn(self, module, input, output):
         """GEGLU variant (:31-61): mask M [4C, C] over the gate half of proj.weight, dense value*act(gate)."""

@@ -4,11 +4,12 @@ hook_fn: out = value * act(gate) (dense GEGLU, natural neuron order); every toke
 and its squares are added to the (t, l) column statistic (utils.TimeLayerColumnNorm, utils.py:344-370); the (t, l)
 counter wraps at n_layers - 1; the output is returned unchanged. MI355X path: sdmoe_linear_geglu +
 sdmoe_colnorm_accum, the statistic stays on the device (no per-call `.cpu()` copy); get_column_norms() returns
-fp16 CPU tensors like the reference's. Text-encoder hooks (hook_module='text') are outside this tier.
+fp16 CPU tensors like the reference's. hook_module='text' (:14-18, :59-71): one ColumnNormCalculator per CLIP
+encoder layer over act(fc1 x) rows; fc1 + act run as one GEMM, the MLP output is fc2 of the same activations.
 """
 from __future__ import annotations
 
-from sdmoe.discovery import TimeLayerColumnNorm
+from sdmoe.discovery import ColumnNormCalculator, TimeLayerColumnNorm
 
 from neuron_receivers.base_receiver import GEGLU, BaseNeuronReceiver
 
@@ -18,9 +19,12 @@ class Wanda(BaseNeuronReceiver):
         super().__init__(seed, replace_fn, keep_nsfw, hook_module, **kw)
         self.T = T
         self.n_layers = n_layers
-        if hook_module != 'unet':
-            raise NotImplementedError("Wanda text-encoder statistics are outside this tier")
-        self.predictivity = TimeLayerColumnNorm(T, n_layers)
+        if hook_module == 'unet':
+            self.predictivity = TimeLayerColumnNorm(T, n_layers)
+        elif hook_module == 'text':
+            self.predictivity = {l: ColumnNormCalculator() for l in range(n_layers)}
+        else:
+            raise ValueError(f"hook_module must be 'unet' or 'text', got {hook_module!r}")
         self.timestep = 0
         self.layer = 0
 
@@ -40,3 +44,12 @@ class Wanda(BaseNeuronReceiver):
         self.predictivity.update(out.reshape(-1, out.shape[-1]), self.timestep, self.layer)
         self.update_time_layer()
         return out
+
+    def text_hook_fn(self, module, input, output):
+        x = input[0]
+        a = module.hidden(x.reshape(-1, x.shape[-1]))
+        if self.layer < self.n_layers:
+            self.predictivity[self.layer].add_rows(a)
+        out = module.fc2.run(a)
+        self.update_time_layer()
+        return out.view(*x.shape[:-1], out.shape[-1])

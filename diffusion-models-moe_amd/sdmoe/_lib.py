@@ -41,6 +41,8 @@ SIGNATURES = {
     "sdmoe_union_over_time": [_P, _L, _I, _L, _F, _P, _P],
     "sdmoe_softmax_rows": [_P, _L, _P, _L, _I, _I, _P],
     "sdmoe_transpose": [_P, _L, _P, _L, _I, _I, _P],
+    "sdmoe_gather_rows": [_P, _L, _P, _I, _I, _P, _L, _I, _P, _L, _P],
+    "sdmoe_attention_short": [_P, _L, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _F, _I, _P],
     "sdmoe_timestep_embedding_rows": [_P, _L, _P, _I, _I, _I, _I, _F, _P],
     "sdmoe_prepare_input": [_P, _P, _I, _I, _L, _I, _P],
     "sdmoe_cfg_ddim_step": [_P, _L, _P, _I, _I, _I, _F, _F, _F, _P, _L, _P],

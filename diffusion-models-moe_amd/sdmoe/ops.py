@@ -13,8 +13,8 @@ import torch
 
 from . import _lib
 
-ACT_NONE, ACT_SILU, ACT_GELU, ACT_RELU = 0, 1, 2, 3
-ACT_BY_NAME = {"none": ACT_NONE, "silu": ACT_SILU, "gelu": ACT_GELU, "relu": ACT_RELU}
+ACT_NONE, ACT_SILU, ACT_GELU, ACT_RELU, ACT_QUICK_GELU = 0, 1, 2, 3, 4
+ACT_BY_NAME = {"none": ACT_NONE, "silu": ACT_SILU, "gelu": ACT_GELU, "relu": ACT_RELU, "quick_gelu": ACT_QUICK_GELU}
 
 
 def _stream():
@@ -498,4 +498,42 @@ def add(a, b, out=None):
         out = torch.empty_like(a)
     st = lib.sdmoe_add(_dev(a, "a"), _dev(b, "b"), _dev(out, "out"), a.numel(), _stream())
     _lib.check(st, "sdmoe_add")
+    return out
+
+
+def gather_rows(table, idx, *, add=None, period=0, out=None):
+    """out[r] = table[idx[r]] (+ add[r % period]) — token + position embedding, pooled-row gather
+    (sdmoe_gather_rows). idx: int32 device tensor [R]."""
+    lib = _lib.load()
+    tp, ldt = _rows(table, "table")
+    C = table.shape[1]
+    R = idx.numel()
+    if out is None:
+        out = torch.empty((R, C), dtype=torch.float16, device=table.device)
+    op, ldo = _rows(out, "out")
+    ap, lda = (None, 0) if add is None else _rows(add, "add")
+    if add is not None and period <= 0:
+        period = add.shape[0]
+    st = lib.sdmoe_gather_rows(tp, ldt, _dev(idx, "idx", torch.int32), R, C, ap, lda, int(period), op, ldo,
+                               _stream())
+    _lib.check(st, "sdmoe_gather_rows")
+    return out
+
+
+def attention_short(q, k, v, nseq, N, heads, out=None, scale=None, causal=True):
+    """Short-sequence (N <= 128) attention per (sequence, head), optional causal mask (sdmoe_attention_short)."""
+    lib = _lib.load()
+    qp, ldq = _rows(q, "q")
+    kp, ldk = _rows(k, "k")
+    vp, ldv = _rows(v, "v")
+    C = q.shape[1]
+    d = C // heads
+    if out is None:
+        out = torch.empty((nseq * N, C), dtype=torch.float16, device=q.device)
+    op, ldo = _rows(out, "out")
+    if scale is None:
+        scale = d ** -0.5
+    st = lib.sdmoe_attention_short(qp, ldq, kp, ldk, vp, ldv, op, ldo, nseq, N, heads, d, float(scale),
+                                   int(bool(causal)), _stream())
+    _lib.check(st, "sdmoe_attention_short")
     return out

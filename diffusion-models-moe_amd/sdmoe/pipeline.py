@@ -115,7 +115,8 @@ class PipelineOutput:
 
 class StableDiffusionPipeline:
     def __init__(self, unet: UNet2DConditionModel, device="cuda", num_inference_steps=50, guidance_scale=7.5,
-                 scheduler="ddim", vae=None):
+                 scheduler="ddim", vae=None, text_encoder=None, tokenizer=None, text_encoder_2=None,
+                 tokenizer_2=None):
         if scheduler not in ("ddim", "pndm"):
             raise ValueError(f"scheduler must be 'ddim' or 'pndm', got {scheduler!r}")
         self.scheduler = scheduler  # "pndm": the reference's default (51 U-Net calls per 50 steps)
@@ -127,6 +128,11 @@ class StableDiffusionPipeline:
         self.prompt_offset = 0  # global index of the first prompt (data-parallel shards set this per rank)
         self.vae = vae  # sdmoe.vae.AutoencoderKLDecoder or None (output_type "pt"/"np" then decodes the latents)
         self.output_type = "latent"  # default of __call__'s output_type (the receivers call pipe(prompt) bare)
+        # sdmoe.clip.CLIPTextModel(s) or None (None: seeded synthetic [77, dim] conditioning, prompt_embedding)
+        self.text_encoder = text_encoder
+        self.tokenizer = tokenizer
+        self.text_encoder_2 = text_encoder_2
+        self.tokenizer_2 = tokenizer_2
 
     @classmethod
     def synthetic(cls, cfg: UNetConfig | None = None, seed: int = 0, device="cuda", **kw):
@@ -138,20 +144,44 @@ class StableDiffusionPipeline:
     def is_sdxl(self):
         return self.config.addition_embed_type == "text_time"
 
-    def encode_prompt(self, prompts):
+    def _ids(self, tok, texts):
+        return tok(texts, padding="max_length", max_length=CTX_LEN, truncation=True, return_tensors="pt").input_ids
+
+    def encode_prompt(self, prompts, return_pooled=False):
         """[uncond x B ; cond x B] context rows [2B*77, dim] fp16 on device (uncond first, as diffusers).
-        SDXL base sets force_zeros_for_empty_prompt: the unconditional embeddings are zeros."""
+        SDXL base sets force_zeros_for_empty_prompt: the unconditional embeddings are zeros.
+        With text encoders: SD-1.x runs text_encoder on [""] * B + prompts (last_hidden_state); SDXL writes the
+        two encoders' penultimate hidden states straight into the two column halves of the context and takes
+        text_encoder_2's projected pooled output (diffusers StableDiffusionXLPipeline.encode_prompt)."""
         dim = self.config.cross_attention_dim
+        B = len(prompts)
+        if self.text_encoder is not None:
+            ctx = torch.empty((2 * B * CTX_LEN, dim), dtype=torch.float16, device=self.device)
+            pooled = None
+            if not self.is_sdxl:
+                self.text_encoder.encode(self._ids(self.tokenizer, [""] * B + list(prompts)), out=ctx)
+            else:
+                d1 = self.text_encoder.config.hidden_size
+                ctx[:B * CTX_LEN].zero_()
+                cond = ctx[B * CTX_LEN:]
+                self.text_encoder.encode(self._ids(self.tokenizer, prompts), hidden_layer=-2, out=cond[:, :d1])
+                r = self.text_encoder_2.encode(self._ids(self.tokenizer_2 or self.tokenizer, prompts),
+                                               hidden_layer=-2, out=cond[:, d1:], pooled=True)
+                pooled = torch.zeros((2 * B, r["text_embeds"].shape[1]), dtype=torch.float16, device=self.device)
+                pooled[B:] = r["text_embeds"]
+            return (ctx, pooled) if return_pooled else ctx
         unc = torch.zeros(CTX_LEN, dim) if self.is_sdxl else prompt_embedding("", dim)
         embs = [unc] * len(prompts) + [prompt_embedding(p, dim) for p in prompts]
-        return torch.cat(embs, 0).to(self.device, torch.float16).contiguous()
+        ctx = torch.cat(embs, 0).to(self.device, torch.float16).contiguous()
+        return (ctx, None) if return_pooled else ctx
 
-    def added_cond(self, prompts):
+    def added_cond(self, prompts, pooled=None):
         """SDXL added_cond_kwargs rows [uncond x B ; cond x B]: pooled text_embeds [2B, pooled] and time_ids
         [2B, 6] (1024^2 uncropped at sample_size 128)."""
         cfg = self.config
         d = cfg.pooled_dim
-        pooled = torch.stack([torch.zeros(d)] * len(prompts) + [pooled_embedding(p, d) for p in prompts])
+        if pooled is None:
+            pooled = torch.stack([torch.zeros(d)] * len(prompts) + [pooled_embedding(p, d) for p in prompts])
         px = 8 * cfg.sample_size
         tids = torch.tensor([sdxl_time_ids(px, px)] * (2 * len(prompts)), dtype=torch.float32)
         return {"text_embeds": pooled, "time_ids": tids}
@@ -172,10 +202,10 @@ class StableDiffusionPipeline:
             latents = torch.cat([initial_latents(seed, prompt_offset + i, cfg) for i in range(B)])
         lat = latents.to(self.device, torch.float32).contiguous()
         ncopy = 2 if do_cfg else 1
-        ctx = self.encode_prompt(prompts)
+        ctx, pooled = self.encode_prompt(prompts, return_pooled=True)
         add_hidden = None
         if self.is_sdxl:
-            ac = self.added_cond(prompts)
+            ac = self.added_cond(prompts, pooled)
             add_hidden = self.unet.add_embed_hidden(ac["text_embeds"], ac["time_ids"])  # once per call
             if not do_cfg:
                 add_hidden = add_hidden[B:]

@@ -25,6 +25,7 @@ extern "C" {
 #define SDMOE_ACT_SILU 1
 #define SDMOE_ACT_GELU 2 /* exact erf GELU, diffusers GEGLU.gelu / F.gelu */
 #define SDMOE_ACT_RELU 3 /* relufied U-Net, sparsity/relufy_model.py:8-15 */
+#define SDMOE_ACT_QUICK_GELU 4 /* x*sigmoid(1.702x), CLIP ViT-L text encoder MLP (transformers ACT2FN['quick_gelu']) */
 
 const char* sdmoe_version(void);
 
@@ -195,6 +196,21 @@ int sdmoe_union_over_time(const void* bits, long t_stride_bytes, int T, long nby
  */
 int sdmoe_softmax_rows(const void* X, long ldx, void* Y, long ldy, int R, int N, void* stream);
 int sdmoe_transpose(const void* X, long ldx, void* Y, long ldy, int R, int C, void* stream);
+
+/*
+ * CLIP text encoder helpers (transformers CLIPTextModel, external — the pipelines' text_encoder
+ * and the reference's hook_module='text' seam, base_receiver.py:59-65, remove_wanda_neurons_fast.py:114-120).
+ * sdmoe_gather_rows — out[r, :C] = table[idx[r], :C] (+ add[r % period, :C] when add != NULL), fp16, C % 8 == 0.
+ *   Replaces CLIPTextEmbeddings (token_embedding(ids) + position_embedding(arange)) and the pooled-output gather
+ *   last_hidden_state[arange(B), eos_position].
+ * sdmoe_attention_short — O = softmax(Q K^T * scale [+ causal mask]) V per (sequence, head) for N <= 128 tokens,
+ *   head_dim <= 128 (% 8); same operand layout as sdmoe_attention. Replaces CLIPAttention with the causal mask of
+ *   CLIPTextTransformer (_create_4d_causal_attention_mask).
+ */
+int sdmoe_gather_rows(const void* table, long ld_table, const int* idx, int R, int C, const void* add, long ld_add,
+                      int period, void* out, long ld_out, void* stream);
+int sdmoe_attention_short(const void* Q, long ldq, const void* K, long ldk, const void* V, long ldv, void* O,
+                          long ldo, int nseq, int N, int heads, int head_dim, float scale, int causal, void* stream);
 
 /* diffusers get_timestep_embedding for one timestep (t_dev if non-NULL, else t), fp16 [dim]. */
 int sdmoe_timestep_embedding(void* out, const float* t_dev, float t, int dim, int flip_sin_to_cos, float freq_shift,
