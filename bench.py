@@ -50,7 +50,11 @@ def parse():
                    help="down: the top-k mask is applied by the down projection as it reads the GEGLU product "
                         "(sdmoe_linear_keep); pass: a separate masking pass over the product (A/B reference)")
     p.add_argument("--decode", action="store_true",
-                   help="also run the VAE decoder inside the timed step (end-to-end images; the metric excludes it)")
+                   help="also run the CLIP text encoder and the VAE decoder inside the timed step (end-to-end "
+                        "images; the metric excludes them, SURVEY §8d)")
+    p.add_argument("--e2e-steps", type=int, default=1,
+                   help="after the timed metric run, time this many end-to-end steps (text encoder + denoise + VAE "
+                        "decode to RGB) and report them as 'end_to_end' (0: skip)")
     p.add_argument("--no-roofline", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-evals", type=int, default=2, help="CPU oracle U-Net evaluations to time")
@@ -93,10 +97,22 @@ def build(args, world, rank, dev):
     cfg = UNetConfig.sdxl(128) if args.model == "sdxl" else UNetConfig.sd14(64)
     pipe = StableDiffusionPipeline.synthetic(cfg, seed=0, device=dev, num_inference_steps=args.inference_steps,
                                              scheduler=args.scheduler)
-    if args.decode:
+    e2e = None
+    if args.decode or (args.e2e_steps > 0 and args.model == "sd14"):
+        from sdmoe.clip import attach_text_encoders
         from sdmoe.vae import AutoencoderKLDecoder, VAEConfig, make_vae_state_dict
-        pipe.vae = AutoencoderKLDecoder(make_vae_state_dict(VAEConfig.sd14(), 0), VAEConfig.sd14(), dev)
-        pipe.output_type = "pt"
+        vae = AutoencoderKLDecoder(make_vae_state_dict(VAEConfig.sd14(), 0), VAEConfig.sd14(), dev)
+        attach_text_encoders(pipe, seed=0)
+        e2e = (pipe.text_encoder, vae)
+
+    def set_e2e(on):
+        """end-to-end mode: CLIP text encoder in front, VAE decode to RGB behind; off: the metric's workload
+        (synthetic context, latents out)."""
+        pipe.text_encoder = e2e[0] if on else None
+        pipe.vae = e2e[1] if on else None
+        pipe.output_type = "pt" if on else "latent"
+    if e2e is not None:
+        set_e2e(args.decode)
     find_and_change_geglu(pipe.unet)                  # relufied U-Net (config 2/3)
     moefy_synthetic(pipe, args.topk, 20, seed=0)      # E = 4C/20 experts, k = int(E*topk)
     geglus = [m for n, m in pipe.unet.named_modules() if n.endswith("ff.net.0")]
@@ -134,7 +150,7 @@ def build(args, world, rank, dev):
         for t in range(T):
             for l in range(len(downs)):
                 wanda._dev[(t, l)] = bits[t][l]
-    return cfg, pipe, rec, wanda
+    return cfg, pipe, rec, wanda, (set_e2e if e2e is not None else None)
 
 
 class KernelTimer:
@@ -234,7 +250,7 @@ def main():
     import sdmoe.unet as U
     _lib.load()
     U.FUSED_KEEP = args.topk_mask == "down"
-    cfg, pipe, rec, wanda = build(args, world, rank, dev)
+    cfg, pipe, rec, wanda, set_e2e = build(args, world, rank, dev)
     # global prompt list: rank r takes its contiguous shard (per-prompt seeds use the global index)
     from sdmoe import distributed as D
     prompts = [f"synthetic prompt {i}" for i in range(world * args.batch)]
@@ -283,6 +299,27 @@ def main():
     images = world * args.batch * args.steps
     value = images / elapsed
 
+    end_to_end = None
+    if set_e2e is not None and not args.decode and args.e2e_steps > 0:
+        set_e2e(True)
+        one_step()  # warm the encoder / decoder shapes
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.e2e_steps):
+            rgb = one_step()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        if world > 1:
+            dist.barrier()
+        el2 = D.max_over_ranks(t1 - t0, dev)
+        set_e2e(False)
+        end_to_end = {"value": round(world * args.batch * args.e2e_steps / el2, 4), "unit": "images/s",
+                      "steps": args.e2e_steps, "ms_per_step": round(el2 / args.e2e_steps * 1e3, 2),
+                      "what": "CLIP ViT-L text encoder (synthetic tokenizer) + the metric's denoise + VAE decode "
+                              "to 512^2 RGB", "outputs_finite": all(bool(torch.isfinite(x).all()) for x in rgb)}
+
     roof = None
     if not args.no_roofline:
         n, ms, flops = timer.result()
@@ -311,11 +348,11 @@ def main():
                                    f"{' + union Wanda mask' if args.mask == 'union' else ''}, "
                                    f"{8 * cfg.sample_size}^2 (4x{cfg.sample_size}x{cfg.sample_size} latents), "
                                    f"{args.inference_steps} {args.scheduler.upper()} steps, CFG 7.5"
-                                   f"{' + VAE decode to 512^2 RGB' if args.decode else ''}",
+                                   f"{' + CLIP text encoder + VAE decode to 512^2 RGB' if args.decode else ''}",
                        "prompts_per_gpu": args.batch, "global_batch": world * args.batch,
                        "parallelism": f"dp{world}"},
             "step_mfma_frac": round(value / world * TFLOP_PER_IMAGE[args.model] / PEAK_FP16_TFLOPS, 4),
-            "roofline": roof, "cpu_baseline": cpu, "outputs_finite": finite,
+            "roofline": roof, "cpu_baseline": cpu, "outputs_finite": finite, "end_to_end": end_to_end,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
