@@ -12,10 +12,10 @@ tail -1 gpurun_out/r1_bench.log | cut -c1-400
 timeout -k 10 300 python tools/op_breakdown.py > gpurun_out/r1_breakdown.log 2>&1 || { tail -20 gpurun_out/r1_breakdown.log; exit 1; }
 head -12 gpurun_out/r1_breakdown.log
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/r1_prof -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline > $R/gpurun_out/r1_prof_bench.log 2>&1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/r1_prof -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --e2e-steps 0 > $R/gpurun_out/r1_prof_bench.log 2>&1
 tail -1 $R/gpurun_out/r1_prof_bench.log | cut -c1-300
-timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/r1_pmcf -o run --output-format csv -- python3 $R/bench.py --inference-steps 2 --steps 1 --warmup 0 --no-cpu-baseline --no-roofline > $R/gpurun_out/r1_pmcf.log 2>&1
-timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/r1_pmcw -o run --output-format csv -- python3 $R/bench.py --inference-steps 2 --steps 1 --warmup 0 --no-cpu-baseline --no-roofline > $R/gpurun_out/r1_pmcw.log 2>&1
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/r1_pmcf -o run --output-format csv -- python3 $R/bench.py --inference-steps 2 --steps 1 --warmup 0 --no-cpu-baseline --no-roofline --e2e-steps 0 > $R/gpurun_out/r1_pmcf.log 2>&1
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/r1_pmcw -o run --output-format csv -- python3 $R/bench.py --inference-steps 2 --steps 1 --warmup 0 --no-cpu-baseline --no-roofline --e2e-steps 0 > $R/gpurun_out/r1_pmcw.log 2>&1
 cd $R
 python tools/prof_summary.py $(find gpurun_out/r1_prof -name '*kernel_stats.csv' | head -1) 40 > gpurun_out/r1_prof_summary.txt
 head -20 gpurun_out/r1_prof_summary.txt
