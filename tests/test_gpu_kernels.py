@@ -151,8 +151,11 @@ def test_forced_tiles(tile):
         _lib.check(lib.sdmoe_tune(1, 0), "tune")
 
 
-@pytest.mark.parametrize("C,HW,eps", [(320, 4096, 1e-5), (960, 256, 1e-6), (2560, 64, 1e-5), (1920, 1024, 1e-5)])
+@pytest.mark.parametrize("C,HW,eps", [(320, 4096, 1e-5), (960, 256, 1e-6), (2560, 64, 1e-5), (1920, 1024, 1e-5),
+                                      (1280, 64, 1e-5), (1280, 256, 1e-5), (640, 1024, 1e-6), (320, 1024, 1e-5),
+                                      (640, 2048, 1e-5), (128, 16, 1e-6)])
 def test_groupnorm_stats(C, HW, eps):
+    """HW <= 1024 takes the single-launch gn_small_kernel, larger HW the partial + finalize pair."""
     nimg = 2
     x = rnd(nimg * HW, C, seed=34) * 2 + 3  # non-zero mean exercises the shifted sums
     gamma, beta = rnd(C, scale=0.1, seed=35) + 1, rnd(C, scale=0.1, seed=36)
@@ -160,6 +163,19 @@ def test_groupnorm_stats(C, HW, eps):
     xn = x.float().view(nimg, HW, C) * sc[:, None, :] + sh[:, None, :]
     ref = F.group_norm(x.float().view(nimg, HW, C).permute(0, 2, 1), 32, gamma.float(), beta.float(), eps)
     close(xn, ref.permute(0, 2, 1), tol=2e-3)
+
+
+def test_groupnorm_stats_channel_slice():
+    """A channel slice of a wider buffer (the zero-copy skip concatenation), small and large paths."""
+    for HW in (256, 4096):
+        nimg, C = 2, 640
+        buf = rnd(nimg * HW, C + 320, seed=40) * 2 - 1
+        x = buf[:, 320:]
+        gamma, beta = rnd(C, scale=0.1, seed=41) + 1, rnd(C, scale=0.1, seed=42)
+        sc, sh = ops.groupnorm_stats(x, nimg, HW, gamma, beta, 1e-5, 32)
+        xn = x.float().reshape(nimg, HW, C) * sc[:, None, :] + sh[:, None, :]
+        ref = F.group_norm(x.float().reshape(nimg, HW, C).permute(0, 2, 1), 32, gamma.float(), beta.float(), 1e-5)
+        close(xn, ref.permute(0, 2, 1), tol=2e-3)
 
 
 @pytest.mark.parametrize("C", [320, 640, 1280])
