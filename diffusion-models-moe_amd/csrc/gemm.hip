@@ -508,6 +508,8 @@ int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
 int dispatch_geglu(const GemmParams& p, hipStream_t s) {
   const int nt320 = ((p.M + 255) / 256) * (p.N / 320);
   const int nt160_128 = ((p.M + 127) / 128) * (p.N / 160);
+  if (g_tile == 1) return launch_tile<128, 160, 2, 2, MODE_GEGLU>(p, nullptr, 0, s);
+  if (g_tile == 4) return launch_tile<256, 160, 4, 2, MODE_GEGLU>(p, nullptr, 0, s);
   if (p.N % 320 == 0 && nt320 >= 240) {
     if (g_tile == 3) return launch_tile<256, 320, 2, 4, MODE_GEGLU>(p, nullptr, 0, s);
     return launch_tile<256, 320, 4, 2, MODE_GEGLU>(p, nullptr, 0, s);  // wave rows of 160 B: 32-B aligned stores
