@@ -24,6 +24,7 @@ SIGNATURES = {
     "sdmoe_groupnorm_apply": [_P, _L, _I, _I, _I, _P, _P, _I, _P, _L, _P],
     "sdmoe_mask_weight": [_P, _P, _L, _L, _P, _P],
     "sdmoe_groupnorm_stats": [_P, _L, _I, _I, _I, _I, _P, _P, _F, _P, _P, _P, _L, _P],
+    "sdmoe_groupnorm": [_P, _L, _I, _I, _I, _I, _P, _P, _F, _I, _P, _L, _P, _P, _P, _L, _P],
     "sdmoe_layernorm": [_P, _L, _P, _L, _I, _I, _P, _P, _F, _P],
     "sdmoe_attention": [_P, _L, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _I, _F, _P],
     "sdmoe_geglu_route": [_P, _L, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _L, _P, _L, _P, _P, _P],

@@ -176,6 +176,24 @@ def groupnorm_stats(x, nimg, HW, gamma, beta, eps, groups=32):
     return scale, shift
 
 
+def groupnorm(x, nimg, HW, gamma, beta, eps, groups=32, silu=False, out=None):
+    """act(GroupNorm(x)) as a new [nimg*HW, C] fp16 tensor (sdmoe_groupnorm: statistics + apply)."""
+    lib = _lib.load()
+    xp, ldx = _rows(x, "x")
+    C = x.shape[1]
+    scale = torch.empty((nimg, C), dtype=torch.float32, device=x.device)
+    shift = torch.empty((nimg, C), dtype=torch.float32, device=x.device)
+    if out is None:
+        out = torch.empty((x.shape[0], C), dtype=torch.float16, device=x.device)
+    op, ldy = _rows(out, "out")
+    ws = _gn_workspace(x.device, nimg * groups * 64 * 2)
+    st = lib.sdmoe_groupnorm(xp, ldx, nimg, HW, C, groups, _dev(gamma, "gamma"), _dev(beta, "beta"), float(eps),
+                             int(bool(silu)), op, ldy, scale.data_ptr(), shift.data_ptr(), ws.data_ptr(), ws.numel(),
+                             _stream())
+    _lib.check(st, "sdmoe_groupnorm")
+    return out
+
+
 def layernorm(x, gamma, beta, eps=1e-5, out=None):
     lib = _lib.load()
     xp, ldx = _rows(x, "x")

@@ -83,6 +83,10 @@ class Norm(nn.Module):
     def stats(self, x2d, nimg, HW):
         return ops.groupnorm_stats(x2d, nimg, HW, self.weight, self.bias, self.eps, self.groups)
 
+    def normalize(self, x2d, nimg, HW, silu):
+        """act(GroupNorm(x)) as a new tensor (sdmoe_groupnorm: statistics + apply in one ABI call)."""
+        return ops.groupnorm(x2d, nimg, HW, self.weight, self.bias, self.eps, self.groups, silu)
+
 
 def act_code(fn):
     """Map a GEGLU `.gelu` callable to the kernel's activation code (diffusers gelu or the relufied ReLU)."""
@@ -335,8 +339,7 @@ class Transformer2DModel(nn.Module):
         self.proj_out = proj_out
 
     def run(self, x, nimg, HW, ctx2d, out):
-        sc, sh = self.norm.stats(x, nimg, HW)
-        hs = self.proj_in.run(x, gn=(sc, sh, False), rows_per_batch=HW)
+        hs = self.proj_in.run(self.norm.normalize(x, nimg, HW, False))
         for blk in self.transformer_blocks:
             hs = blk.run(hs, nimg, HW, ctx2d)
         return self.proj_out.run(hs, residual=x, out=out)
@@ -351,17 +354,16 @@ class ResnetBlock2D(nn.Module):
 
     def run(self, x, nimg, H, W, temb_all, out):
         HW = H * W
-        sc1, sh1 = self.norm1.stats(x, nimg, HW)
+        xn = self.norm1.normalize(x, nimg, HW, True)
         o, n = self.temb_slice
         # temb_all: [1, sum Cout] (SD-1.x, one timestep embedding for the batch) or [nimg, sum Cout] (SDXL:
         # per-image text_time conditioning) -> per-image column add in the conv epilogue
         bstride = temb_all.stride(0) if temb_all.shape[0] > 1 else 0
-        h = ops.conv3x3(x, nimg, H, W, self.conv1.weight, self.conv1.bias, gn=(sc1, sh1, True),
+        h = ops.conv3x3(xn, nimg, H, W, self.conv1.weight, self.conv1.bias,
                         coladd=temb_all[:, o:o + n], coladd_bstride=bstride)
-        sc2, sh2 = self.norm2.stats(h, nimg, HW)
+        hn = self.norm2.normalize(h, nimg, HW, True)
         res = x if self.conv_shortcut is None else self.conv_shortcut.run(x)
-        return ops.conv3x3(h, nimg, H, W, self.conv2.weight, self.conv2.bias, gn=(sc2, sh2, True), residual=res,
-                           out=out)
+        return ops.conv3x3(hn, nimg, H, W, self.conv2.weight, self.conv2.bias, residual=res, out=out)
 
 
 class Sampler(nn.Module):
@@ -625,10 +627,10 @@ class UNet2DConditionModel(nn.Module):
                         final = o
 
         # ---- out
-        sc, sh = self.conv_norm_out.stats(final, nimg, H * W)
+        fn = self.conv_norm_out.normalize(final, nimg, H * W, True)
         if out is None:
             out = new(nimg * H * W, OUT_PAD)
-        return ops.conv3x3(final, nimg, H, W, self.conv_out.weight, self.conv_out.bias, gn=(sc, sh, True), out=out)
+        return ops.conv3x3(fn, nimg, H, W, self.conv_out.weight, self.conv_out.bias, out=out)
 
     def forward(self, sample, timestep, encoder_hidden_states, added_cond_kwargs=None):
         """diffusers-style call: sample [n, 4, H, W], encoder_hidden_states [n, 77, ctx]; returns eps [n,4,H,W].

@@ -73,6 +73,16 @@ int sdmoe_groupnorm_stats(const void* X, long ldx, int nimg, int HW, int C, int 
                           const void* beta, float eps, float* scale, float* shift, float* workspace,
                           long workspace_floats, void* stream);
 
+/*
+ * GroupNorm (+SiLU) in one call: Y = act(X * scale + shift) with the statistics of sdmoe_groupnorm_stats (scale /
+ * shift are written too), i.e. sdmoe_groupnorm_stats followed by sdmoe_groupnorm_apply. Y must not alias X. Same
+ * workspace as _stats.
+ * Replaces: GroupNorm(+SiLU) in front of ResnetBlock2D conv1/conv2, Transformer2DModel.proj_in, conv_norm_out.
+ */
+int sdmoe_groupnorm(const void* X, long ldx, int nimg, int HW, int C, int groups, const void* gamma, const void* beta,
+                    float eps, int silu, void* Y, long ldy, float* scale, float* shift, float* workspace,
+                    long workspace_floats, void* stream);
+
 /* LayerNorm over the last dimension (C % 64 == 0, C <= 2048). Replaces BasicTransformerBlock norm1/2/3. */
 int sdmoe_layernorm(const void* X, long ldx, void* Y, long ldy, int M, int C, const void* gamma, const void* beta,
                     float eps, void* stream);

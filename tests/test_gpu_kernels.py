@@ -165,6 +165,25 @@ def test_groupnorm_stats(C, HW, eps):
     close(xn, ref.permute(0, 2, 1), tol=2e-3)
 
 
+@pytest.mark.parametrize("C,HW,silu", [(1280, 64, True), (640, 1024, False), (2560, 256, True), (320, 4096, True),
+                                       (960, 2048, False)])
+def test_groupnorm_fused_apply(C, HW, silu):
+    """sdmoe_groupnorm: statistics + apply(+SiLU) in one ABI call, small (HW <= 1024) and large statistics paths."""
+    nimg = 3
+    buf = rnd(nimg * HW, C + 64, seed=46) * 2 + 1
+    x = buf[:, 64:]
+    gamma, beta = rnd(C, scale=0.1, seed=47) + 1, rnd(C, scale=0.1, seed=48)
+    y = ops.groupnorm(x, nimg, HW, gamma, beta, 1e-5, 32, silu)
+    ref = F.group_norm(x.float().reshape(nimg, HW, C).permute(0, 2, 1), 32, gamma.float(), beta.float(), 1e-5)
+    ref = ref.permute(0, 2, 1).reshape(nimg * HW, C)
+    if silu:
+        ref = F.silu(ref)
+    close(y, ref, tol=5e-3)
+    sc, sh = ops.groupnorm_stats(x, nimg, HW, gamma, beta, 1e-5, 32)
+    ap = ops.groupnorm_apply(x, nimg, HW, sc, sh, silu)
+    assert (y.float() - ap.float()).abs().max().item() <= 2e-3 * max(1.0, ap.float().abs().max().item())
+
+
 def test_groupnorm_stats_channel_slice():
     """A channel slice of a wider buffer (the zero-copy skip concatenation), small and large paths."""
     for HW in (256, 4096):
