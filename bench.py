@@ -326,7 +326,7 @@ def main():
         if n:
             achieved = flops / (ms / 1e3) / 1e12
             traffic = None
-            if args.traffic and os.path.exists(args.traffic):
+            if args.traffic and os.path.exists(args.traffic) and args.model == "sd14":  # PMC file is the SD-1.4 run
                 traffic = json.load(open(args.traffic)).get("bytes_per_launch")
             roof = {"bound": "mfma", "kernel": "sdmoe_conv3x3: implicit-GEMM conv (gemm_kernel<BM,BN,MODE=1|2,STAGES>"
                                                " + split-K reduce where used)",
@@ -339,7 +339,8 @@ def main():
         cpu = cpu_baseline(args)
     if rank == 0:
         line = {
-            "metric": "images/sec SD-1.4 512² 50-step DDIM, expert mask on; 1→8 GPU scaling",
+            "metric": ("images/sec SD-1.4 512² 50-step DDIM, expert mask on; 1→8 GPU scaling" if args.model == "sd14"
+                       else "images/sec SDXL-base 1024² 50-step DDIM, expert mask on (config 5)"),
             "value": round(value, 4), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp16", "data": "synthetic",
