@@ -127,3 +127,49 @@ def test_text_hook_seam_module_names_cpu():
     hooks = r2.register_hooks(P)
     assert all(h is not None for h in hooks) and len(hooks) == 12
     r2.remove_hooks(hooks)
+
+
+GOLDEN = {"clip_quick_gelu_legacy": CLIPTextConfig.tiny(64, 2, 2),
+          "clip_gelu_proj": CLIPTextConfig(hidden_size=64, intermediate_size=256, num_hidden_layers=2,
+                                           num_attention_heads=2, hidden_act="gelu", projection_dim=32,
+                                           eos_token_id=49407, pad_token_id=0)}
+
+
+@pytest.mark.parametrize("name", sorted(GOLDEN))
+def test_oracle_vs_reference_text_goldens(name, golden_dir):
+    """Committed fixtures (tests/golden/make_clip_golden.py): transformers' CLIPTextModel outputs and the
+    REFERENCE's own text_hook_fn bodies (remove_wanda_neurons_fast.py:85-101, wanda_receiver.py:59-71) run on
+    transformers' CLIPMLP — the oracle reproduces all of them without transformers or the reference present."""
+    import os
+    import numpy as np
+    from oracle import hooks_ref  # noqa: F401  (oracle package import check)
+    from sdmoe import mask_io
+    g = np.load(os.path.join(golden_dir, f"{name}.npz"))
+    cfg = GOLDEN[name]
+    sd = make_clip_state_dict(cfg, int(g["seed"]))
+    ids = torch.from_numpy(g["ids"])
+    assert torch.equal(ids, SyntheticCLIPTokenizer(pad_token_id=cfg.pad_token_id)(
+        ["a photo of a cat", "", "The Starry Night, a painting by Vincent van Gogh",
+         "nude figure, oil on canvas"]).input_ids)
+    hs, last, pooled, te = CR.encode_ref(ids, sd, cfg)
+    torch.testing.assert_close(last, torch.from_numpy(g["last"]), atol=2e-5, rtol=1e-5)
+    torch.testing.assert_close(torch.stack(hs), torch.from_numpy(g["hidden"]), atol=2e-5, rtol=1e-5)
+    if cfg.projection_dim:
+        torch.testing.assert_close(te, torch.from_numpy(g["text_embeds"]), atol=2e-5, rtol=1e-5)
+    else:
+        torch.testing.assert_close(pooled, torch.from_numpy(g["pooled"]), atol=2e-5, rtol=1e-5)
+    h = torch.from_numpy(g["hook_h"])
+    L, F = cfg.num_hidden_layers, cfg.intermediate_size
+    for l in range(L):
+        p = f"text_model.encoder.layers.{l}.mlp"
+        mask = torch.from_numpy(mask_io.unpack_mask(g["hook_mask_bits"][l], F).astype(np.float32))
+        torch.testing.assert_close(CR.wanda_remove_text_hook(h, sd, p, cfg.hidden_act, mask),
+                                   torch.from_numpy(g["remove_out"][l]), atol=1e-5, rtol=1e-5)
+        rows = []
+        for rep in range(2):
+            r, out = CR.wanda_text_stats(h * (1.0 + rep), sd, p, cfg.hidden_act)
+            rows.append(r)
+            torch.testing.assert_close(out, torch.from_numpy(g["wanda_out"][rep * L + l]), atol=1e-5, rtol=1e-5)
+        torch.testing.assert_close(torch.cat(rows).norm(dim=0), torch.from_numpy(g["wanda_norms"][l]),
+                                   atol=1e-5, rtol=1e-5)
+    assert list(g["remove_counter"]) == [1, 0]  # one hooked call per layer wraps the (t, l) counter once

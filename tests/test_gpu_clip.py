@@ -223,3 +223,39 @@ def test_text_hook_wanda_stats_vs_oracle():
         got = rec.predictivity[l].get_column_norms().float()
         exp = rows[l].norm(dim=0)
         assert rel_l2(got, exp) <= 1e-2, l
+
+
+@pytest.mark.parametrize("name", ["clip_quick_gelu_legacy", "clip_gelu_proj"])
+def test_text_hooks_vs_reference_goldens(name, golden_dir):
+    """Our HIP receivers' text_hook_fn vs the REFERENCE's own text_hook_fn outputs (tests/golden/make_clip_golden.py,
+    computed in fp32 on transformers' CLIPMLP): fp16 storage, rel-L2 <= 1e-2; the encoder vs transformers' outputs."""
+    import os
+    import numpy as np
+    from neuron_receivers import Wanda, WandaRemoveNeuronsFast
+    from test_clip_oracle import GOLDEN
+    g = np.load(os.path.join(golden_dir, f"{name}.npz"))
+    cfg = GOLDEN[name]
+    sd = make_clip_state_dict(cfg, int(g["seed"]))
+    enc = CLIPTextModel.from_state_dict(sd, cfg, DEV)
+    ids = torch.from_numpy(g["ids"])
+    r = enc.encode(ids, pooled=True)
+    B, L_, C = g["last"].shape
+    assert rel_l2(r["hidden"], torch.from_numpy(g["last"]).reshape(B * L_, C)) <= 1e-2
+    key = "text_embeds" if cfg.projection_dim else "pooled"
+    assert rel_l2(r[key], torch.from_numpy(g[key])) <= 2e-2
+    L = cfg.num_hidden_layers
+    mlps = [enc.text_model.encoder.layers[l].mlp for l in range(L)]
+    h = torch.from_numpy(g["hook_h"]).half().to(DEV)
+    rm = WandaRemoveNeuronsFast.from_packed(0, {0: {l: g["hook_mask_bits"][l] for l in range(L)}}, 1, L,
+                                            hook_module='text')
+    for l in range(L):
+        out = rm.text_hook_fn(mlps[l], (h,), None)
+        assert rel_l2(out, torch.from_numpy(g["remove_out"][l])) <= 1e-2, l
+    assert [rm.timestep, rm.layer] == list(g["remove_counter"])
+    w = Wanda(0, 1, L, hook_module='text')
+    for rep in range(2):
+        for l in range(L):
+            out = w.text_hook_fn(mlps[l], (h * (1.0 + rep),), None)
+            assert rel_l2(out, torch.from_numpy(g["wanda_out"][rep * L + l])) <= 1e-2
+    for l in range(L):
+        assert rel_l2(w.predictivity[l].get_column_norms(), torch.from_numpy(g["wanda_norms"][l])) <= 1e-2
