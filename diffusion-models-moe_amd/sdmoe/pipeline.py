@@ -3,11 +3,15 @@ denoising loop entirely on the GPU (U-Net on the sdmoe kernels, CFG + DDIM updat
 
 Call shape kept from diffusers / the reference's callers: `pipe(prompt_or_list, safety_checker=...)` returns
 an object with `.images` (base_receiver.py:73, remove_wanda_neurons_fast.py:127-130, eval_coco.py:266-272).
-The CLIP text encoder and the VAE decoder are outside this tier: prompts map to seeded
-synthetic [77, 768] embeddings and `.images` holds the final latents ([4, H, W] fp32 per prompt).
+Without `text_encoder` / `vae` attached (the metric's workload) prompts map to seeded synthetic
+[77, 768] embeddings and `.images` holds the final latents ([4, H, W] fp32 per prompt); with them attached
+(sdmoe.clip, sdmoe.vae) prompts are encoded by the HIP CLIP encoder and `output_type` "pt" / "np" decodes to RGB.
+Loop invariants are hoisted per call: the cross-attention K/V of the context (unet.Attention.cross_kv) and the
+projected time embeddings of every step of the schedule (UNet2DConditionModel.time_embed_table).
 """
 from __future__ import annotations
 
+import os
 import zlib
 from dataclasses import dataclass
 
@@ -18,6 +22,9 @@ from . import ops
 from .config import UNetConfig
 from .unet import CTX_LEN, IN_PAD, OUT_PAD, UNet2DConditionModel
 from .weights import make_state_dict
+
+# all steps' time embeddings in one batched pass per call (0: per step, the A/B reference)
+PRECOMPUTE_TEMB = os.environ.get("SDMOE_TEMB_TABLE", "1") != "0"
 
 
 def ddim_schedule(num_inference_steps=50, num_train_timesteps=1000, beta_start=0.00085, beta_end=0.012,
@@ -215,16 +222,22 @@ class StableDiffusionPipeline:
         x_in = torch.zeros((ncopy * B * HW, IN_PAD), dtype=torch.float16, device=self.device)
         eps = torch.empty((ncopy * B * HW, OUT_PAD), dtype=torch.float16, device=self.device)
         ops.prepare_input(lat, x_in, ncopy)
+        def temb_row(table, i):
+            return None if table is None else table[i:i + 1]
+        time_table = self.unet.time_embed_table if PRECOMPUTE_TEMB else (lambda ts: None)
         if self.scheduler == "pndm":
             hist = torch.zeros((4,) + tuple(lat.shape), dtype=torch.float32, device=self.device)
             cur = torch.zeros_like(lat)
-            for t, coef, flags in pndm_schedule(steps):
-                self.unet.forward_nhwc(x_in, float(t), ctx, out=eps, add_hidden=add_hidden)
+            plan = pndm_schedule(steps)
+            table = time_table([t for t, _, _ in plan])  # loop-invariant: all steps at once
+            for i, (t, coef, flags) in enumerate(plan):
+                self.unet.forward_nhwc(x_in, float(t), ctx, out=eps, add_hidden=add_hidden, temb=temb_row(table, i))
                 ops.cfg_multistep_step(eps, lat, do_cfg, g, hist, cur, coef, flags, next_in=x_in)
         else:
             ts, a_t, a_prev = ddim_schedule(steps)
+            table = time_table(list(ts))  # loop-invariant: all steps at once
             for s, t in enumerate(ts):
-                self.unet.forward_nhwc(x_in, float(t), ctx, out=eps, add_hidden=add_hidden)
+                self.unet.forward_nhwc(x_in, float(t), ctx, out=eps, add_hidden=add_hidden, temb=temb_row(table, s))
                 ops.cfg_ddim_step(eps, lat, do_cfg, g, a_t[s], a_prev[s], next_in=x_in)
         return PipelineOutput(images=self._finish(lat, output_type or self.output_type))
 

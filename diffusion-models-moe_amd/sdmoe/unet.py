@@ -532,7 +532,24 @@ class UNet2DConditionModel(nn.Module):
             e = self.time_embedding.linear_2.run(e, act=ops.ACT_SILU)  # every consumer applies SiLU(temb) first
         return ops.linear(e, self.temb_w, self.temb_b)
 
-    def forward_nhwc(self, x_in, t, ctx2d, out=None, t_dev=None, add_hidden=None):
+    def time_embed_table(self, ts):
+        """SD-1.x: the projected time embeddings of a whole schedule at once — [len(ts), sum Cout] fp16, row s =
+        time_embed(ts[s]) — as three M = len(ts) GEMMs instead of len(ts) GEMV chains (the 20160 x 1280 fused
+        ResNet projection is read once per pipeline call, not once per step). None for SDXL (its per-step half
+        depends on the per-image micro-conditioning)."""
+        cfg = self.config
+        if cfg.addition_embed_type == "text_time":
+            return None
+        dev = self.conv_in.weight.device
+        t_dev = torch.tensor([float(t) for t in ts], dtype=torch.float32, device=dev)
+        d = cfg.block_out_channels[0]
+        e = torch.empty((len(ts), d), dtype=torch.float16, device=dev)
+        ops.timestep_embedding_rows(t_dev, d, e, flip_sin_to_cos=cfg.flip_sin_to_cos, freq_shift=cfg.freq_shift)
+        e = self.time_embedding.linear_1.run(e, act=ops.ACT_SILU)
+        e = self.time_embedding.linear_2.run(e, act=ops.ACT_SILU)
+        return ops.linear(e, self.temb_w, self.temb_b)
+
+    def forward_nhwc(self, x_in, t, ctx2d, out=None, t_dev=None, add_hidden=None, temb=None):
         """One U-Net evaluation. x_in: [nimg*H*W, 64] fp16 (channels 0..3 = latent), ctx2d: [nimg*77, ctx dim].
         add_hidden (SDXL): add_embed_hidden(text_embeds, time_ids). Returns eps as [nimg*H*W, 8] fp16
         (channels 0..3 valid)."""
@@ -543,7 +560,8 @@ class UNet2DConditionModel(nn.Module):
         ch = cfg.block_out_channels
         nblk = len(ch)
         L = cfg.layers_per_block
-        temb_all = self.time_embed(t, t_dev, add_hidden)
+        # temb: this step's row of time_embed_table (precomputed for the pipeline call's schedule), else per step
+        temb_all = temb if temb is not None else self.time_embed(t, t_dev, add_hidden)
 
         # ---- plan the up-path concat buffers [rows, C_prev + C_skip] (consumption order)
         rev = list(reversed(ch))
