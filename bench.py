@@ -64,10 +64,16 @@ def parse():
 
 
 def setup_dist(n):
+    """One process per GPU over RCCL ("nccl"). SDMOE_SAME_DEVICE_REHEARSAL=1 (rehearsal of the N > 1 code path on a
+    one-GPU box, never used for a measurement): every rank on cuda:0, gloo collectives."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world > 1 and os.environ.get("SDMOE_SAME_DEVICE_REHEARSAL") == "1":
+        local = 0
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo")
+    elif world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
@@ -352,7 +358,10 @@ def main():
                                    f"{' + CLIP text encoder + VAE decode to 512^2 RGB' if args.decode else ''}",
                        "prompts_per_gpu": args.batch, "global_batch": world * args.batch,
                        "parallelism": f"dp{world}"},
-            "step_mfma_frac": round(value / world * TFLOP_PER_IMAGE[args.model] / PEAK_FP16_TFLOPS, 4),
+            # TFLOP_PER_IMAGE is quoted for 50 U-Net calls; scale to this run's call count
+            "step_mfma_frac": round(value / world * TFLOP_PER_IMAGE[args.model] *
+                                    (args.inference_steps + (1 if args.scheduler == "pndm" else 0)) / 50 /
+                                    PEAK_FP16_TFLOPS, 4),
             "roofline": roof, "cpu_baseline": cpu, "outputs_finite": finite, "end_to_end": end_to_end,
         }
         print(json.dumps(line), flush=True)
