@@ -340,7 +340,8 @@ int sdmoe_attn_set_nqf(int v) {
 extern "C" int sdmoe_attention(const void* Q, long ldq, const void* K, long ldk, const void* V, long ldv,
                                void* O, long ldo, int nimg, int Nq, int Nk, int heads, int head_dim,
                                float scale, void* stream) {
-  if (!Q || !K || !V || !O || nimg <= 0 || Nq <= 0 || Nk <= 0 || heads <= 0) return SDMOE_EARG;
+  if (nimg == 0 || Nq == 0) return SDMOE_OK;  // empty batch / no queries: nothing to write
+  if (!Q || !K || !V || !O || nimg < 0 || Nq < 0 || Nk <= 0 || heads <= 0) return SDMOE_EARG;
   if (ldq % 8 || ldk % 8 || ldv % 8 || ldo % 4) return SDMOE_ESHAPE;
   AttnParams p{(const half_t*)Q, ldq, (const half_t*)K, ldk, (const half_t*)V, ldv, (half_t*)O, ldo,
                Nq, Nk, heads, scale * 1.4426950408889634f};

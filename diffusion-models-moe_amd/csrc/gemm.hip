@@ -609,8 +609,8 @@ extern "C" int sdmoe_linear(const void* A, long lda, const void* W, long ldw, co
                             const void* coladd, long coladd_bstride, int rows_per_batch,
                             const void* R, long ldr, void* C, long ldc, int M, int N, int K, int act,
                             float* workspace, long workspace_floats, void* stream) {
-  if (!A || !W || !C || M < 0 || N <= 0 || K <= 0) return SDMOE_EARG;
   if (M == 0) return SDMOE_OK;
+  if (!A || !W || !C || M < 0 || N <= 0 || K <= 0) return SDMOE_EARG;
   if (K % 64 || N % 8 || lda % 8 || ldw % 8 || ldc % 8 || (R && ldr % 8)) return SDMOE_ESHAPE;
   if (coladd && rows_per_batch <= 0) return SDMOE_EARG;
   GemmParams p{};
@@ -628,8 +628,8 @@ extern "C" int sdmoe_linear(const void* A, long lda, const void* W, long ldw, co
 extern "C" int sdmoe_linear_keep(const void* A, long lda, const void* keep, const void* W, long ldw, const void* bias,
                                  const void* R, long ldr, void* C, long ldc, int M, int N, int K, float* workspace,
                                  long workspace_floats, void* stream) {
-  if (!A || !keep || !W || !C || M < 0 || N <= 0 || K <= 0) return SDMOE_EARG;
   if (M == 0) return SDMOE_OK;
+  if (!A || !keep || !W || !C || M < 0 || N <= 0 || K <= 0) return SDMOE_EARG;
   if (K % 64 || N % 8 || lda % 8 || ldw % 8 || ldc % 8 || (R && ldr % 8)) return SDMOE_ESHAPE;
   GemmParams p{};
   p.A = (const half_t*)A; p.lda = lda; p.W = (const half_t*)W; p.ldw = ldw;
@@ -645,8 +645,8 @@ extern "C" int sdmoe_linear_keep(const void* A, long lda, const void* keep, cons
 extern "C" int sdmoe_linear_geglu(const void* A, long lda, const void* W, long ldw, const void* bias, void* P,
                                   long ldp, int M, int F, int K, int act, void* score, long ld_score, int esize,
                                   void* stream) {
-  if (!A || !W || !bias || !P || M < 0 || F <= 0 || K <= 0) return SDMOE_EARG;
   if (M == 0) return SDMOE_OK;
+  if (!A || !W || !bias || !P || M < 0 || F <= 0 || K <= 0) return SDMOE_EARG;
   if (K % 64 || F % 80 || lda % 8 || ldw % 8 || ldp % 8) return SDMOE_ESHAPE;
   if (score && (esize <= 0 || 40 % esize || ld_score < F / esize)) return SDMOE_ESHAPE;
   if (!(act == ACT_GELU || act == ACT_RELU || act == ACT_NONE || act == ACT_SILU)) return SDMOE_EUNSUP;
@@ -665,7 +665,8 @@ extern "C" int sdmoe_conv3x3(const void* X, long ldx, int nimg, int H, int W, in
                              const void* Wt, const void* bias, const void* coladd, long coladd_bstride,
                              const void* R, long ldr, void* Y, long ldy, int Cout, int stride, int upsample,
                              int act, float* workspace, long workspace_floats, void* stream) {
-  if (!X || !Wt || !Y || nimg <= 0 || H <= 0 || W <= 0 || Cout <= 0) return SDMOE_EARG;
+  if (nimg == 0) return SDMOE_OK;
+  if (!X || !Wt || !Y || nimg < 0 || H <= 0 || W <= 0 || Cout <= 0) return SDMOE_EARG;
   if (Cin % 64 || Cout % 8 || ldx % 8 || ldy % 8 || (R && ldr % 8)) return SDMOE_ESHAPE;
   if (!(stride == 1 || stride == 2) || (upsample && stride != 1)) return SDMOE_EUNSUP;
   GemmParams p{};

@@ -308,8 +308,8 @@ int launch_topk(half_t* P, long ldp, int M, int F, int E, int esize, int k, cons
 
 extern "C" int sdmoe_moe_topk_mask(void* P, long ldp, int M, int F, int E, int esize, int k, const void* score,
                                    long ld_score, const unsigned* removed_bits, unsigned* sel_out, void* stream) {
-  if (!P || !score || M < 0 || F <= 0 || E <= 0 || esize <= 0) return SDMOE_EARG;
   if (M == 0) return SDMOE_OK;
+  if (!P || !score || M < 0 || F <= 0 || E <= 0 || esize <= 0) return SDMOE_EARG;
   if (F % 8 || ldp % 8 || E * esize != F || ld_score < E) return SDMOE_ESHAPE;
   if (E > 256) return SDMOE_EUNSUP;
   if (k < 0 || k > E) return SDMOE_EARG;
@@ -319,8 +319,8 @@ extern "C" int sdmoe_moe_topk_mask(void* P, long ldp, int M, int F, int E, int e
 
 extern "C" int sdmoe_moe_topk_keep(int M, int F, int E, int esize, int k, const void* score, long ld_score,
                                    const unsigned* removed_bits, void* keep, unsigned* sel_out, void* stream) {
-  if (!keep || !score || M < 0 || F <= 0 || E <= 0 || esize <= 0) return SDMOE_EARG;
   if (M == 0) return SDMOE_OK;
+  if (!keep || !score || M < 0 || F <= 0 || E <= 0 || esize <= 0) return SDMOE_EARG;
   if (F % 64 || E * esize != F || ld_score < E) return SDMOE_ESHAPE;
   if (E > 256 || esize > 40) return SDMOE_EUNSUP;
   if (k < 0 || k > E) return SDMOE_EARG;
@@ -332,8 +332,8 @@ extern "C" int sdmoe_geglu_route(const void* Y, long ldy, int M, int F, int E, i
                                  const int* e_off, const int* e_nid, const unsigned* removed_bits, void* out,
                                  long ldo, void* gate_out, long ldg, unsigned* sel_out, void* score_out,
                                  void* stream) {
-  if (!Y || !out || M < 0 || F <= 0 || E < 0) return SDMOE_EARG;
   if (M == 0) return SDMOE_OK;
+  if (!Y || !out || M < 0 || F <= 0 || E < 0) return SDMOE_EARG;
   if (F % 8 || ldy % 8 || ldo % 8 || (gate_out && ldg % 8)) return SDMOE_ESHAPE;
   if (E > 256) return SDMOE_EUNSUP;
   if (E > 0 && (!labels || !e_off || !e_nid || k < 0 || k > E)) return SDMOE_EARG;

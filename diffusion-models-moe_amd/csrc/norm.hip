@@ -296,8 +296,8 @@ extern "C" int sdmoe_groupnorm(const void* X, long ldx, int nimg, int HW, int C,
 
 extern "C" int sdmoe_layernorm(const void* X, long ldx, void* Y, long ldy, int M, int C, const void* gamma,
                                const void* beta, float eps, void* stream) {
-  if (!X || !Y || !gamma || !beta || M < 0 || C <= 0) return SDMOE_EARG;
   if (M == 0) return SDMOE_OK;
+  if (!X || !Y || !gamma || !beta || M < 0 || C <= 0) return SDMOE_EARG;
   if (C % 64 || ldx % 8 || ldy % 8 || C > 2048) return SDMOE_ESHAPE;
   hipStream_t s = (hipStream_t)stream;
   // 32-row blocks while that still gives >= ~4 blocks per CU, else one-wave 8-row blocks

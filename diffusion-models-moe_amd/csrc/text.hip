@@ -100,8 +100,8 @@ __global__ __launch_bounds__(256) void attention_short_kernel(const half_t* __re
 
 extern "C" int sdmoe_gather_rows(const void* table, long ld_table, const int* idx, int R, int C, const void* add,
                                  long ld_add, int period, void* out, long ld_out, void* stream) {
-  if (!table || !idx || !out || R < 0 || C <= 0) return SDMOE_EARG;
   if (R == 0) return SDMOE_OK;
+  if (!table || !idx || !out || R < 0 || C <= 0) return SDMOE_EARG;
   if (C % 8 || ld_table % 8 || ld_out % 8 || (add && (ld_add % 8 || period <= 0))) return SDMOE_ESHAPE;
   const long work = (long)R * (C / 8);
   gather_rows_kernel<<<(unsigned)((work + 255) / 256), 256, 0, (hipStream_t)stream>>>(
@@ -113,8 +113,8 @@ extern "C" int sdmoe_gather_rows(const void* table, long ld_table, const int* id
 extern "C" int sdmoe_attention_short(const void* Q, long ldq, const void* K, long ldk, const void* V, long ldv,
                                      void* O, long ldo, int nseq, int N, int heads, int head_dim, float scale,
                                      int causal, void* stream) {
-  if (!Q || !K || !V || !O || nseq < 0 || N <= 0 || heads <= 0 || head_dim <= 0) return SDMOE_EARG;
   if (nseq == 0) return SDMOE_OK;
+  if (!Q || !K || !V || !O || nseq < 0 || N <= 0 || heads <= 0 || head_dim <= 0) return SDMOE_EARG;
   if (N > SHORT_MAXN || head_dim > SHORT_MAXD || head_dim % 8 || ldq % 2 || ldk % 2 || ldv % 8)
     return SDMOE_ESHAPE;
   attention_short_kernel<<<nseq * heads, 256, 0, (hipStream_t)stream>>>(

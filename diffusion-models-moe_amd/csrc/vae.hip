@@ -71,8 +71,8 @@ __global__ __launch_bounds__(256) void transpose_kernel(const half_t* __restrict
 }  // namespace
 
 extern "C" int sdmoe_softmax_rows(const void* X, long ldx, void* Y, long ldy, int R, int N, void* stream) {
-  if (!X || !Y || R < 0 || N <= 0) return SDMOE_EARG;
   if (R == 0) return SDMOE_OK;
+  if (!X || !Y || R < 0 || N <= 0) return SDMOE_EARG;
   if (N % 8 || ldx % 8 || ldy % 8 || N > 8192) return SDMOE_ESHAPE;
   hipStream_t s = (hipStream_t)stream;
   const int blocks = (R + 3) / 4;
@@ -87,8 +87,8 @@ extern "C" int sdmoe_softmax_rows(const void* X, long ldx, void* Y, long ldy, in
 }
 
 extern "C" int sdmoe_transpose(const void* X, long ldx, void* Y, long ldy, int R, int C, void* stream) {
-  if (!X || !Y || R < 0 || C < 0) return SDMOE_EARG;
   if (R == 0 || C == 0) return SDMOE_OK;
+  if (!X || !Y || R < 0 || C < 0) return SDMOE_EARG;
   const dim3 grid((C + 63) / 64, (R + 63) / 64);
   transpose_kernel<<<grid, 256, 0, (hipStream_t)stream>>>((const half_t*)X, ldx, (half_t*)Y, ldy, R, C);
   SDMOE_CHECK_LAUNCH();

@@ -10,7 +10,9 @@
  *   - `stream` is a hipStream_t (pass torch.cuda.current_stream().cuda_stream); every call is asynchronous,
  *     allocates nothing, never synchronises and is safe under hipGraph stream capture;
  *   - return 0 on success, >0 a hipError_t from the launch, <0 an argument error:
- *     -1 bad pointer/size, -2 unsupported shape/alignment, -3 unsupported mode.
+ *     -1 bad pointer/size, -2 unsupported shape/alignment, -3 unsupported mode;
+ *   - an empty problem (zero rows / images / sequences) is a no-op that returns 0 before any pointer is checked
+ *     (an empty framework tensor may carry a NULL data pointer).
  *   The library neither frees nor retains caller buffers.
  */
 #ifndef SDMOE_H
