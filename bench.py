@@ -246,6 +246,15 @@ def cpu_baseline(args):
                       f"{dt:.2f} s each, x{args.inference_steps} steps per image"}
 
 
+def metric_label(args):
+    """BASELINE.json's metric string for the default run (SD-1.4, 50 DDIM steps); other runs say what they ran."""
+    sched = f"{args.inference_steps}-step {args.scheduler.upper()}"
+    if args.model == "sdxl":
+        return f"images/sec SDXL-base 1024² {sched}, expert mask on (config 5)"
+    mask = {"remove": "expert mask on", "union": "expert mask + union Wanda mask on", "none": "no mask"}[args.mask]
+    return f"images/sec SD-1.4 512² {sched}, {mask}; 1→8 GPU scaling"
+
+
 def main():
     args = parse()
     if args.batch is None:
@@ -260,7 +269,6 @@ def main():
     # global prompt list: rank r takes its contiguous shard (per-prompt seeds use the global index)
     from sdmoe import distributed as D
     prompts = [f"synthetic prompt {i}" for i in range(world * args.batch)]
-    mine, offset = D.shard(prompts, rank, world)
 
     timer = KernelTimer("conv3x3_launch")
     if not args.no_roofline:
@@ -268,18 +276,15 @@ def main():
     pipe.unet.conv_in.weight._sdmoe_conv_in = True
     pipe.unet.conv_out.weight._sdmoe_conv_out = True
 
-    pipe.prompt_offset = offset  # global prompt index of this rank's first prompt (seeds its latents)
-
     def one_step():
-        """One batch through the reference receiver API: observe_activation(pipe, prompts)."""
+        """One batch through the reference receiver API: this rank's shard of the global prompt list (seeded by
+        global prompt index) through observe_activation(pipe, prompts) (sdmoe.distributed.run_shard)."""
         hooks = []
         if wanda is not None:
             wanda.reset_time_layer()
             hooks = wanda.register_hooks(pipe)
         try:
-            if hasattr(rec, "reset_time_layer"):
-                rec.reset_time_layer()
-            out, _ = rec.observe_activation(pipe, mine)
+            out, _ = D.run_shard(pipe, rec, prompts, rank, world)
         finally:
             if wanda is not None:
                 wanda.remove_hooks(hooks)
@@ -345,8 +350,7 @@ def main():
         cpu = cpu_baseline(args)
     if rank == 0:
         line = {
-            "metric": ("images/sec SD-1.4 512² 50-step DDIM, expert mask on; 1→8 GPU scaling" if args.model == "sd14"
-                       else "images/sec SDXL-base 1024² 50-step DDIM, expert mask on (config 5)"),
+            "metric": metric_label(args),
             "value": round(value, 4), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp16", "data": "synthetic",

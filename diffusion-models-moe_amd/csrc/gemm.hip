@@ -51,10 +51,14 @@ struct GemmParams {
   half_t* score; long ld_score;
   int esize;
   int prio;  // experiment knob: raise wave priority around the MFMA block
-  // expert keep mask of the A operand (MODE_KEEP): keep[(k / 64) * M * 8 + m * 8 + (k % 64) / 8] bit (k % 8) =
-  // neuron k of token m survives the top-k; the A fragments are ANDed with it after their LDS read
+  // expert keep mask of the A operand (MODE_KEEP / MODE_KEEPW): keep[(k / 64) * M * 8 + m * 8 + (k % 64) / 8] bit
+  // (k % 8) = neuron k of token m survives the top-k; the A fragments are ANDed with it after their LDS read
   const uint8_t* keep;
   int keep_bytes;
+  // Wanda weight mask of the W operand (MODE_WMASK / MODE_KEEPW), the same K-step-major layout over W's rows:
+  // wmask[(k / 64) * N * 8 + n * 8 + (k % 64) / 8] bit (k % 8) SET = W[n, k] removed (zeroed on the B fragments)
+  const uint8_t* wmask;
+  int wmask_bytes;
 };
 
 SDMOE_DEV int swz(int row) { return (row >> 1) & 7; }
@@ -93,13 +97,20 @@ SDMOE_DEV void epilogue8(const GemmParams& p, int m, int n, float (&v)[8]) {
   *reinterpret_cast<half8*>(p.C + (long)m * p.ldc + n) = o;
 }
 
-// GEGLU: GEMM loads, routed-GEGLU epilogue; KEEP: GEMM whose A operand is masked per (row, neuron) by keep bits
-enum { MODE_GEMM = 0, MODE_CONV = 1, MODE_CONV_UP = 2, MODE_GEGLU = 3, MODE_KEEP = 4 };
+// GEGLU: GEMM loads, routed-GEGLU epilogue; KEEP: GEMM whose A operand is masked per (row, neuron) by keep bits;
+// WMASK: W operand masked per (row, k) by Wanda bits; KEEPW: both (the routed FFN down projection under a Wanda mask)
+enum { MODE_GEMM = 0, MODE_CONV = 1, MODE_CONV_UP = 2, MODE_GEGLU = 3, MODE_KEEP = 4, MODE_WMASK = 5, MODE_KEEPW = 6 };
+constexpr bool mode_akeep(int mode) { return mode == MODE_KEEP || mode == MODE_KEEPW; }
+constexpr bool mode_wmask(int mode) { return mode == MODE_WMASK || mode == MODE_KEEPW; }
 
-// LDS bytes one ring stage holds besides the A/B tiles: the keep bytes of the tile's rows for one 64-deep K-step
-// (MODE_KEEP: BM rows x 8 bytes, whole 1-KiB LDS-DMA pieces)
+// LDS bytes one ring stage holds besides the A/B tiles: the mask bytes of the tile's rows for one 64-deep K-step
+// (A keep: BM rows x 8 bytes; W mask: BN rows x 8 bytes; each in whole 1-KiB LDS-DMA pieces)
 template <int BM, int MODE>
-constexpr int keep_stage_bytes() { return MODE == MODE_KEEP ? ((BM * 8 + 1023) / 1024) * 1024 : 0; }
+constexpr int keep_a_bytes() { return mode_akeep(MODE) ? ((BM * 8 + 1023) / 1024) * 1024 : 0; }
+template <int BN, int MODE>
+constexpr int keep_w_bytes() { return mode_wmask(MODE) ? ((BN * 8 + 1023) / 1024) * 1024 : 0; }
+template <int BM, int BN, int MODE>
+constexpr int keep_stage_bytes() { return keep_a_bytes<BM, MODE>() + keep_w_bytes<BN, MODE>(); }
 constexpr int KEEP_LUT_BYTES = 16 * 8;  // 4 keep bits -> 4 x 16-bit lane masks
 
 // Routed-GEGLU epilogue over one staged pass (rows x WN fp32 in LDS, row stride WN_PAD) of a wave's tile
@@ -189,7 +200,8 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
   auto swzk = [](int row) { return (row >> 1) & (CPRW - 1); };  // conflict-free b128 fragment reads
   constexpr bool CONV = MODE == MODE_CONV || MODE == MODE_CONV_UP;
   constexpr bool GEGLU = MODE == MODE_GEGLU;
-  constexpr bool KEEP = MODE == MODE_KEEP;
+  constexpr bool AKEEP = mode_akeep(MODE), WKEEP = mode_wmask(MODE);
+  constexpr bool KEEP = AKEEP || WKEEP;
   static_assert(!KEEP || BKT == 64, "keep bytes are laid out per 64-deep K-step");
   constexpr int NW = WMW * WNW;                  // waves per workgroup
   constexpr int WM = BM / WMW, WN = BN / WNW;    // per-wave output tile
@@ -197,14 +209,16 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
   static_assert(WM % 16 == 0 && WN % 16 == 0, "wave tile must be whole 16x16 fragments");
   constexpr int A_INS = BM / RPP, B_INS = BN / RPP;  // 1-KiB LDS-DMA wave-instructions per stage
   constexpr int A_PW = (A_INS + NW - 1) / NW, B_PW = (B_INS + NW - 1) / NW;
-  constexpr int K_INS = keep_stage_bytes<BM, MODE>() / 1024;  // keep pieces per stage (<= NW)
+  constexpr int KA_INS = keep_a_bytes<BM, MODE>() / 1024;     // A keep pieces per stage
+  constexpr int K_INS = keep_stage_bytes<BM, BN, MODE>() / 1024;  // A keep + W mask pieces per stage (<= NW)
   static_assert(K_INS <= NW, "one keep piece per wave at most");
   constexpr int K_PW = KEEP ? 1 : 0;             // every wave issues one (waves >= K_INS repeat piece 0)
   constexpr int PER_WAVE = A_PW + B_PW + K_PW;   // every wave issues exactly this many (surplus -> dummy slot)
   constexpr int STAGE_AB = (BM + BN) * BK * 2;
   constexpr bool PADDED = (A_PW * NW != A_INS) || (B_PW * NW != B_INS);
   constexpr int KEEP_OFF = STAGE_AB + (PADDED ? 1024 : 0);
-  constexpr int STAGE = KEEP_OFF + keep_stage_bytes<BM, MODE>();
+  constexpr int WKEEP_OFF = KEEP_OFF + keep_a_bytes<BM, MODE>();
+  constexpr int STAGE = KEEP_OFF + keep_stage_bytes<BM, BN, MODE>();
   constexpr int WN_PAD = WN + 4;
   constexpr int NPASS = (NW * (WM / 2) * WN_PAD * 4 <= NSTAGE * STAGE) ? 2 : ((NW * (WM / 4) * WN_PAD * 4 <= NSTAGE * STAGE) ? 4 : 8);
   static_assert(FM % NPASS == 0, "epilogue passes must split the wave's fragment rows");
@@ -273,17 +287,21 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
     bvoff[j] = (j * NW + wave < B_INS && n < p.N) ? (unsigned)((long)n * p.ldw * 2) + (unsigned)((lch ^ swzk(r)) * 16)
                                                   : OOB;
   }
-  // keep pieces (MODE_KEEP): wave w < K_INS stages the keep bytes of tile rows [128 w, 128 w + 128) (16 B = two rows
-  // per lane); the other waves repeat piece 0 -- the same bytes to the same LDS place -- so every wave issues
-  // PER_WAVE instructions per stage and the counted vmcnt waits stay uniform
-  const __amdgpu_buffer_rsrc_t rsK =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.keep, (short)0, KEEP ? p.keep_bytes : 0, 0x00020000);
+  // mask pieces: wave w < KA_INS stages the A keep bytes of tile rows [128 w, 128 w + 128) (16 B = two rows per
+  // lane), waves KA_INS .. K_INS-1 the W mask bytes of tile columns [128 (w - KA_INS), +128); the other waves
+  // repeat piece 0 -- the same bytes to the same LDS place -- so every wave issues PER_WAVE instructions per stage
+  // and the counted vmcnt waits stay uniform
+  const int kpiece = KEEP && wave < K_INS ? wave : 0;
+  const bool kpa = AKEEP && kpiece < KA_INS;  // wave-uniform: this wave's piece is A keep bytes (else W mask bytes)
+  const __amdgpu_buffer_rsrc_t rsK = __builtin_amdgcn_make_buffer_rsrc(
+      kpa ? (void*)p.keep : (void*)p.wmask, (short)0, KEEP ? (kpa ? p.keep_bytes : p.wmask_bytes) : 0, 0x00020000);
+  const unsigned kstride = kpa ? (unsigned)p.M * 8u : (unsigned)p.N * 8u;  // bytes per K-step of the mask layout
   unsigned kvoff = OOB;
   int kdst = KEEP_OFF;
   if constexpr (KEEP) {
-    const int piece = wave < K_INS ? wave : 0;
-    kvoff = (unsigned)((m0 + 128 * piece) * 8 + lane * 16);
-    kdst = KEEP_OFF + piece * 1024;
+    kvoff = kpa ? (unsigned)((m0 + 128 * kpiece) * 8 + lane * 16)
+                : (unsigned)((n0 + 128 * (kpiece - KA_INS)) * 8 + lane * 16);
+    kdst = kpa ? KEEP_OFF + kpiece * 1024 : WKEEP_OFF + (kpiece - KA_INS) * 1024;
     // nibble -> two 16-bit-lane masks: entry e masks halves 0..3 by bits 0..3 of e
     if (tid < 16) {
       const unsigned lo = ((tid & 1) ? 0xFFFFu : 0u) | ((tid & 2) ? 0xFFFF0000u : 0u);
@@ -333,7 +351,7 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
     }
 #pragma unroll
     for (int j = 0; j < B_PW; ++j) bld16(rsW, sa + b_dst(j), bvoff[j], kb);
-    if constexpr (KEEP) bld16(rsK, sa + kdst, kvoff, (unsigned)ks * (unsigned)p.M * 8u);
+    if constexpr (KEEP) bld16(rsK, sa + kdst, kvoff, (unsigned)ks * kstride);
   };
 
   float4v acc[FM][FN];
@@ -375,7 +393,7 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
       for (int i = 0; i < FM; ++i) {
         const int row = wr * WM + i * 16 + fr;
         af[i] = *reinterpret_cast<const half8*>(sa + row * RB + (((kk * 4 + fg) ^ swzk(row)) << 4));
-        if constexpr (KEEP) {  // zero the neurons of this row's dropped experts (8 neurons = chunk kk*4+fg)
+        if constexpr (AKEEP) {  // zero the neurons of this row's dropped experts (8 neurons = chunk kk*4+fg)
           const unsigned kbyte = *reinterpret_cast<const unsigned char*>(sa + KEEP_OFF + row * 8 + kk * 4 + fg);
           const uint2v lo = *reinterpret_cast<const uint2v*>(smem + LUT_OFF + (kbyte & 15u) * 8);
           const uint2v hi = *reinterpret_cast<const uint2v*>(smem + LUT_OFF + (kbyte >> 4) * 8);
@@ -388,6 +406,14 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
       for (int j = 0; j < FN; ++j) {
         const int row = wc * WN + j * 16 + fr;
         bf[j] = *reinterpret_cast<const half8*>(sbm + row * RB + (((kk * 4 + fg) ^ swzk(row)) << 4));
+        if constexpr (WKEEP) {  // zero this W row's Wanda-masked weights (8 k = chunk kk*4+fg); mask bit SET = removed
+          const unsigned mbyte = ~*reinterpret_cast<const unsigned char*>(sa + WKEEP_OFF + row * 8 + kk * 4 + fg);
+          const uint2v lo = *reinterpret_cast<const uint2v*>(smem + LUT_OFF + (mbyte & 15u) * 8);
+          const uint2v hi = *reinterpret_cast<const uint2v*>(smem + LUT_OFF + ((mbyte >> 4) & 15u) * 8);
+          uint4v u = __builtin_bit_cast(uint4v, bf[j]);
+          u[0] &= lo[0]; u[1] &= lo[1]; u[2] &= hi[0]; u[3] &= hi[1];
+          bf[j] = __builtin_bit_cast(half8, u);
+        }
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i)
@@ -483,8 +509,8 @@ int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
     // 4-wave tiles: 2-stage ring (2 workgroups/CU) when the grid has >= ~300 workgroups, else 3-stage; 8-wave
     // tiles: 3-stage where it fits in LDS -- measured crossovers on MI355X.
     const int stages = g_stages ? g_stages : ((WMW * WNW == 4 && ntiles * p.ksplit >= 300) ? 2 : 3);
-    constexpr bool FITS3 = 3 * ((BM + BN) * 64 * 2 + 1024 + keep_stage_bytes<BM, MODE>()) +
-                               (MODE == MODE_KEEP ? KEEP_LUT_BYTES : 0) <= 160 * 1024;
+    constexpr bool FITS3 = 3 * ((BM + BN) * 64 * 2 + 1024 + keep_stage_bytes<BM, BN, MODE>()) +
+                               (keep_stage_bytes<BM, BN, MODE>() ? KEEP_LUT_BYTES : 0) <= 160 * 1024;
     if constexpr (FITS3) {
       if (stages == 2) gemm_kernel<BM, BN, WMW, WNW, MODE, 2, 64><<<grid, NT, 0, s>>>(p);
       else gemm_kernel<BM, BN, WMW, WNW, MODE, 3, 64><<<grid, NT, 0, s>>>(p);
@@ -536,7 +562,7 @@ int dispatch(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
   // 1-1.25 waves of 128x160 tiles (M = 4096 x N = 1280 projections at the 16x16 level): 64x160 tiles double
   // the grid to two workgroups per CU — 15-18 % faster in isolation (tools/gpu_tiles_all.sh). Convs keep their
   // tiles: with the convs included the same-box pipeline A/B measured 0.5 % slower.
-  if ((MODE == MODE_GEMM || MODE == MODE_KEEP) && p.N % 160 == 0 && nt160_128 >= 200 && nt160_128 < 320 &&
+  if ((MODE == MODE_GEMM || MODE >= MODE_KEEP) && p.N % 160 == 0 && nt160_128 >= 200 && nt160_128 < 320 &&
       p.K <= 5120)
     return launch_tile<64, 160, 2, 2, MODE>(p, ws, ws_floats, s);
   if (p.N % 160 == 0 && p.K >= 2560 && nt160_128 < 300 && !(MODE == MODE_CONV && p.stride == 2))
@@ -598,6 +624,29 @@ __global__ __launch_bounds__(256) void mask_weight_kernel(const half_t* __restri
   }
 }
 
+// Wanda bits [N][K/8] (bit k%8 of byte (n, k/8) = W[n, k] removed) -> the GEMM's K-step-major layout
+// out[s][n] (uint64) bit j = mask(n, k = perm ? perm[64 s + j] : 64 s + j): one thread per output word. perm maps a
+// permuted column position to the original column (the routed FFN down projection's expert-major neuron order).
+__global__ __launch_bounds__(256) void wmask_kmajor_kernel(const uint8_t* __restrict__ bits, long ldb, int N, int K,
+                                                           const int* __restrict__ perm, unsigned long long* __restrict__ out) {
+  const long nwords = (long)(K / 64) * N;
+  for (long id = blockIdx.x * 256L + threadIdx.x; id < nwords; id += (long)gridDim.x * 256) {
+    const int s = (int)(id / N), n = (int)(id - (long)s * N);
+    const uint8_t* row = bits + (long)n * ldb;
+    unsigned long long w = 0;
+    if (perm) {
+      for (int j = 0; j < 64; ++j) {
+        const int k = perm[64 * s + j];
+        w |= (unsigned long long)((row[k >> 3] >> (k & 7)) & 1u) << j;
+      }
+    } else {
+#pragma unroll
+      for (int b = 0; b < 8; ++b) w |= (unsigned long long)row[8 * s + b] << (8 * b);
+    }
+    out[id] = w;
+  }
+}
+
 int grid_for(long n) {
   long g = (n + 255) / 256;
   return (int)(g > 4096 ? 4096 : (g < 1 ? 1 : g));
@@ -625,21 +674,35 @@ extern "C" int sdmoe_linear(const void* A, long lda, const void* W, long ldw, co
   return dispatch<MODE_GEMM>(p, workspace, workspace_floats, (hipStream_t)stream);
 }
 
-extern "C" int sdmoe_linear_keep(const void* A, long lda, const void* keep, const void* W, long ldw, const void* bias,
-                                 const void* R, long ldr, void* C, long ldc, int M, int N, int K, float* workspace,
-                                 long workspace_floats, void* stream) {
+extern "C" int sdmoe_linear_masked(const void* A, long lda, const void* keep, const void* W, long ldw,
+                                   const void* wmask, const void* bias, const void* R, long ldr, void* C, long ldc,
+                                   int M, int N, int K, float* workspace, long workspace_floats, void* stream) {
   if (M == 0) return SDMOE_OK;
-  if (!A || !keep || !W || !C || M < 0 || N <= 0 || K <= 0) return SDMOE_EARG;
+  if (!A || !W || !C || M < 0 || N <= 0 || K <= 0) return SDMOE_EARG;
   if (K % 64 || N % 8 || lda % 8 || ldw % 8 || ldc % 8 || (R && ldr % 8)) return SDMOE_ESHAPE;
   GemmParams p{};
   p.A = (const half_t*)A; p.lda = lda; p.W = (const half_t*)W; p.ldw = ldw;
   p.bias = (const half_t*)bias; p.R = (const half_t*)R; p.ldr = ldr; p.C = (half_t*)C; p.ldc = ldc;
   p.M = M; p.N = N; p.K = K; p.act = ACT_NONE; p.rows_per_batch = 1;
-  const long ab = ((long)(M - 1) * lda + K) * 2, wb = ((long)(N - 1) * ldw + K) * 2, kb = (long)(K / 64) * M * 8;
-  if (ab >= (long)OOB || wb >= (long)OOB || kb >= (long)OOB) return SDMOE_ESHAPE;
+  const long ab = ((long)(M - 1) * lda + K) * 2, wb = ((long)(N - 1) * ldw + K) * 2;
+  const long kb = (long)(K / 64) * M * 8, mb = (long)(K / 64) * N * 8;
+  if (ab >= (long)OOB || wb >= (long)OOB || kb >= (long)OOB || mb >= (long)OOB) return SDMOE_ESHAPE;
   p.a_bytes = (int)ab; p.w_bytes = (int)wb;
-  p.keep = (const uint8_t*)keep; p.keep_bytes = (int)kb;
-  return dispatch<MODE_KEEP>(p, workspace, workspace_floats, (hipStream_t)stream);
+  p.keep = (const uint8_t*)keep; p.keep_bytes = keep ? (int)kb : 0;
+  p.wmask = (const uint8_t*)wmask; p.wmask_bytes = wmask ? (int)mb : 0;
+  hipStream_t s = (hipStream_t)stream;
+  if (keep && wmask) return dispatch<MODE_KEEPW>(p, workspace, workspace_floats, s);
+  if (keep) return dispatch<MODE_KEEP>(p, workspace, workspace_floats, s);
+  if (wmask) return dispatch<MODE_WMASK>(p, workspace, workspace_floats, s);
+  return dispatch<MODE_GEMM>(p, workspace, workspace_floats, s);
+}
+
+extern "C" int sdmoe_linear_keep(const void* A, long lda, const void* keep, const void* W, long ldw, const void* bias,
+                                 const void* R, long ldr, void* C, long ldc, int M, int N, int K, float* workspace,
+                                 long workspace_floats, void* stream) {
+  if (M != 0 && !keep) return SDMOE_EARG;
+  return sdmoe_linear_masked(A, lda, keep, W, ldw, nullptr, bias, R, ldr, C, ldc, M, N, K, workspace,
+                             workspace_floats, stream);
 }
 
 extern "C" int sdmoe_linear_geglu(const void* A, long lda, const void* W, long ldw, const void* bias, void* P,
@@ -693,6 +756,16 @@ extern "C" int sdmoe_groupnorm_apply(const void* X, long ldx, int nimg, int HW, 
   const long rows = (long)nimg * HW;
   gn_apply_kernel<<<grid_for(rows * (C / 8)), 256, 0, (hipStream_t)stream>>>(
       (const half_t*)X, ldx, HW, C, scale, shift, silu, (half_t*)Y, ldy, rows);
+  SDMOE_CHECK_LAUNCH();
+  return SDMOE_OK;
+}
+
+extern "C" int sdmoe_wmask_kmajor(const void* bits, long ldb, int N, int K, const int* perm, void* out, void* stream) {
+  if (N == 0) return SDMOE_OK;
+  if (!bits || !out || N < 0 || K <= 0) return SDMOE_EARG;
+  if (K % 64 || ldb < K / 8) return SDMOE_ESHAPE;
+  wmask_kmajor_kernel<<<grid_for((long)(K / 64) * N), 256, 0, (hipStream_t)stream>>>(
+      (const uint8_t*)bits, ldb, N, K, perm, (unsigned long long*)out);
   SDMOE_CHECK_LAUNCH();
   return SDMOE_OK;
 }

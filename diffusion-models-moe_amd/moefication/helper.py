@@ -1,4 +1,4 @@
-"""MoE-fication helpers — drop-in for moefication/helper.py:6-96 of the reference.
+"""MoE-fication helpers — drop-in for moefication/helper.py:48-78 of the reference.
 
 `modify_ffn` turns an expert-label file (moe_utils.ParamSplit output: torch.save(list[int]) of length 4C,
 moe_utils.py:54-61) into `module.patterns` [E, 4C] (0/1, weight dtype/device) and `module.k = int(E * topk)`
@@ -6,6 +6,12 @@ moe_utils.py:54-61) into `module.patterns` [E, 4C] (0/1, weight dtype/device) an
 (:65-78). The device routing layout (labels + per-expert neuron lists) is derived once from these attributes by
 sdmoe.unet.GEGLU.routing(). The offline clustering itself (KMeansConstrained, moe_utils.py:97-107) is outside
 this tier: `balanced_random_labels` is the seeded stand-in used for synthetic runs.
+The template helpers of the offline driver (get_model_block_config / make_templates / test_template,
+helper.py:6-46, used by moefy_sd_model.py) and the frequency counter (initialise_expert_counter, :80-96, used by
+freq_expert_select.py) serve out-of-scope scripts and are not provided: GEGLU layers are found by walking the
+module tree, as modify_ffn_to_experts does.
+Label files hold whatever KMeansConstrained produced -- lists of numpy int32/int64 scalars in the reference's
+own files -- and are read with mask_io.load_labels (torch.load weights_only=True plus the numpy scalar types).
 """
 from __future__ import annotations
 
@@ -14,37 +20,8 @@ import os
 import numpy as np
 import torch
 
+from sdmoe import mask_io
 from sdmoe.unet import GEGLU
-
-
-def get_model_block_config(model_id):
-    config = {}
-    if model_id in ('runwayml/stable-diffusion-v1-5', 'CompVis/stable-diffusion-v1-4', 'sd-1.4'):
-        config['down_blocks'] = {'layer_idx': [0, 1, 2], 'attention_idx': [0, 1]}
-        config['mid_block'] = {'layer_idx': [-1], 'attention_idx': [0]}
-        config['up_blocks'] = {'layer_idx': [1, 2, 3], 'attention_idx': [0, 1, 2]}
-    return config
-
-
-def make_templates(template, config):
-    templates = []
-    for key in config.keys():
-        for layer in config[key]['layer_idx']:
-            if layer == -1:
-                t_ = '{}.attentions.{}.transformer_blocks.0.ff.net.0.proj.weight'
-                for att in config[key]['attention_idx']:
-                    templates.append(t_.format(key, att))
-            else:
-                for att in config[key]['attention_idx']:
-                    templates.append(template % (key, layer, att))
-    return templates
-
-
-def test_template(templates, model):
-    model_ffns = [name + '.proj.weight' for name, m in model.unet.named_modules()
-                  if 'ff.net' in name and isinstance(m, GEGLU)]
-    assert all(ffn in templates for ffn in model_ffns)
-    return True
 
 
 def balanced_random_labels(num_neurons, expert_size, seed):
@@ -61,7 +38,7 @@ def modify_ffn(ffn, path, k, labels=None):
     """helper.py:48-62: labels -> ffn.patterns [E, 4C] (weight dtype/device), ffn.k = int(E * k)."""
     assert isinstance(ffn, GEGLU)
     if labels is None:
-        labels = torch.load(path, weights_only=True)
+        labels = mask_io.load_labels(path)
     labels = np.asarray(labels, dtype=np.int64)
     cluster_num = int(labels.max()) + 1
     patterns = np.stack([labels == i for i in range(cluster_num)]).astype(np.float32)
@@ -97,16 +74,3 @@ def moefy_synthetic(model, topk_experts=0.2, expert_size=20, seed=0):
         nexp[name + '.proj.weight'] = module.patterns.shape[0]
     layer_names.sort()
     return model, layer_names, nexp
-
-
-def initialise_expert_counter(model, timesteps=51):
-    expert_counter = {t: {} for t in range(timesteps)}
-    names = []
-    for name, module in model.unet.named_modules():
-        if 'ff.net' in name and isinstance(module, GEGLU):
-            ffn_name = name + '.proj.weight'
-            for t in range(timesteps):
-                expert_counter[t][ffn_name] = np.zeros(module.patterns.shape[0])
-            names.append(ffn_name)
-    names.sort()
-    return expert_counter, names

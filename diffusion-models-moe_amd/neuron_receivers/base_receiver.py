@@ -31,6 +31,8 @@ class GELU(torch.nn.Module):
 class BaseNeuronReceiver:
     '''Base class for hooking (and changing) the U-Net FFN activations.'''
 
+    _sdmoe_receiver = True  # sdmoe.unet.FeedForward keeps its fused path only under hooks owned by these receivers
+
     def __init__(self, seed=0, replace_fn=GEGLU, keep_nsfw=False, hook_module='unet', store_gates=True):
         self.seed = seed
         self.gates = []

@@ -3,7 +3,13 @@
 One WandaRemoveNeuronsFast per concept plus a union remover whose (t, l) masks are the element-wise OR of the
 selected concepts' masks (:43-53). The snapshot's union step crashes (App. A #6); this restates the intended
 OR, done directly on the bit-packed masks (bitwise OR of packed bytes == element-wise OR of the masks).
-Image stitching (:83-99) is outside this tier: remove_concepts returns the latents.
+As in the reference, the union remover starts from the masks of the LAST configured concept (its constructor
+builds it from the loop's final `path_expert_indx`, :24-33) and keeps OR-ing across calls until
+reset_union_remover() zeroes it (:35-41).
+remove_concepts keeps the reference's two-value contract (:55-99; unified_editing.py:126 unpacks two values):
+(stitched, singles) where `stitched` is [before | after] side by side along the width -- the tensor form of the
+PIL paste at :83-99 (latents, or RGB when the pipeline decodes) -- and `singles` the same pair per concept (None for
+one concept). The unstitched images of the last call are kept in `self.last_outputs`.
 """
 from __future__ import annotations
 
@@ -31,10 +37,11 @@ class MultiConceptRemoverWanda:
                 self.removers[concept] = WandaRemoveNeuronsFast(
                     seed=seed, path_expert_indx=path, T=T, n_layers=n_layers, replace_fn=replace_fn,
                     keep_nsfw=keep_nsfw, remove_timesteps=remove_timesteps, weights_shape=weights_shape)
-        first = next(iter(self.removers.values()))
-        zeros = {t: {l: np.zeros_like(first.mask_bits[t][l]) for l in range(n_layers)} for t in range(T)}
-        self.union_neuron_remover = WandaRemoveNeuronsFast.from_packed(seed, zeros, T, n_layers, replace_fn=replace_fn,
+        last = list(self.removers.values())[-1]  # the reference's union remover loads the last concept's masks
+        start = {t: {l: np.array(last.mask_bits[t][l], copy=True) for l in range(n_layers)} for t in range(T)}
+        self.union_neuron_remover = WandaRemoveNeuronsFast.from_packed(seed, start, T, n_layers, replace_fn=replace_fn,
                                                                        keep_nsfw=keep_nsfw)
+        self.last_outputs = None
 
     def reset_union_remover(self):
         u = self.union_neuron_remover
@@ -51,10 +58,18 @@ class MultiConceptRemoverWanda:
                 for l in range(self.n_layers):
                     u.set_mask_bits(t, l, np.bitwise_or(u.mask_bits[t][l], self.removers[c].mask_bits[t][l]))
 
+    @staticmethod
+    def stitch(before, after):
+        """[before | after] along the last (width) axis: the side-by-side pair of multi_concept_remover.py:83-99."""
+        return torch.cat([before, after], dim=-1)
+
     def remove_concepts(self, model, prompt, concepts):
-        """Returns (latents with the union removed, latents without removal, per-concept latents)."""
+        """Returns (stitched [original | union removed], per-concept stitched pairs or None) -- two values, as the
+        reference. self.last_outputs = {"removal", "original", "singles"} unstitched."""
         if len(concepts) == 0:
-            return model(prompt).images[0], None
+            out = model(prompt).images[0]
+            self.last_outputs = {"removal": None, "original": out, "singles": None}
+            return out, None
         singles = []
         if len(concepts) > 1:
             self.handle_multiple_concepts(concepts)
@@ -69,4 +84,6 @@ class MultiConceptRemoverWanda:
         torch.manual_seed(self.seed)
         np.random.seed(self.seed)
         out_pre = model(prompt).images[0]
-        return out_removal, out_pre, (singles if singles else None)
+        self.last_outputs = {"removal": out_removal, "original": out_pre, "singles": singles or None}
+        stitched_singles = [self.stitch(out_pre, s) for s in singles] if singles else None
+        return self.stitch(out_pre, out_removal), stitched_singles

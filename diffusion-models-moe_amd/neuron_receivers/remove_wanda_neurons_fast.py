@@ -5,8 +5,14 @@ then the (t, l) counter advances. The mask applies at every step (App. A #8); `r
 `weights_shape` are accepted (callers pass them, App. A #5) — weights_shape is used for JSON index masks,
 remove_timesteps is stored but, as in the reference's Fast receiver, not consulted.
 MI355X layout: masks are bit-packed [C, 4C/8] and uploaded once (all (t, l): 316 MB for SD-1.4 at T=51, vs
-~20 GB as dense int64 in the reference); the GEMM zeroes masked weights while staging W tiles, so there is no
-per-call host->device mask copy, no W.clone() and no second GEMM (reference K9).
+~20 GB as dense int64 in the reference), then converted once per (t, l) on the device into the masked GEMM's
+K-step-major layout (sdmoe_wmask_kmajor); sdmoe_linear_masked zeroes the masked weights on the W fragments after
+their LDS read, so there is no per-call host->device mask copy, no W.clone()/masked weight copy and no second GEMM
+(reference K9).
+Under MoE routing (config 4: union Wanda mask on a MoE-fied U-Net) the FeedForward keeps its fused routed path:
+when this receiver is the only hook on ff.net.2 it calls fused_linear(), which applies the same (t, l) mask with
+its columns permuted into the experts' neuron order (converted once per (t, l, layer routing)) together with the
+top-k keep bits, in one sdmoe_linear_masked launch, and advances the counter exactly as linear_hook_fn does.
 The GEGLU variant hook_fn (:31-61, mask over the gate half of proj.weight) uses the same bitmask path, and so does
 the text-encoder variant text_hook_fn (:85-101, hook_module='text': mask M[0][l] over CLIPMLP.fc2).
 """
@@ -60,13 +66,40 @@ class WandaRemoveNeuronsFast(NeuronPredictivity):
 
     def set_mask_bits(self, t, l, bits):
         self.mask_bits[t][l] = np.asarray(bits, dtype=np.uint8)
-        self._dev.pop((t, l), None)
+        # drop the device copy and every layout derived from it (K-major, permuted, GEGLU gate-half forms)
+        for key in [k for k in self._dev if k == (t, l) or (isinstance(k[0], str) and tuple(k[1:3]) == (t, l))]:
+            del self._dev[key]
 
     def device_bits(self, t, l, device):
         d = self._dev.get((t, l))
         if d is None:
             d = self._dev[(t, l)] = torch.from_numpy(np.ascontiguousarray(self.mask_bits[t][l])).to(device)
         return d
+
+    def device_kmajor(self, t, l, device, perm=None):
+        """The (t, l) mask in sdmoe_linear_masked's layout (int64 [4C/64, C]); perm (int32 device [4C], the routed
+        FFN's neuron order) permutes its columns. Converted once per (t, l, perm) on the device and cached."""
+        key = ("kmajor", t, l, None if perm is None else perm.data_ptr())
+        d = self._dev.get(key)
+        if d is None:
+            d = self._dev[key] = ops.wmask_kmajor(self.device_bits(t, l, device), perm)
+        return d
+
+    def _check_shape(self, bits, weight, what):
+        if bits.shape[0] != weight.shape[0] or bits.shape[1] * 8 != weight.shape[1]:
+            raise ValueError(f"{what} mask ({self.timestep},{self.layer}) shape {tuple(bits.shape)} does not match "
+                             f"weight {tuple(weight.shape)}")
+
+    def fused_linear(self, module, x2d, keep, perm, weight_perm, residual):
+        """linear_hook_fn's arithmetic for the fused routed FFN (sdmoe.unet.FeedForward): x2d is the GEGLU product in
+        the experts' neuron order perm (int32 device [4C]), keep its top-k keep bits (or None), weight_perm
+        ff.net.2's weight with its columns in that order. Returns y + residual; advances the (t, l) counter."""
+        bits = self.device_bits(self.timestep, self.layer, module.weight.device)
+        self._check_shape(bits, module.weight, "ff.net.2")
+        wm = self.device_kmajor(self.timestep, self.layer, module.weight.device, perm)
+        y = ops.linear_masked(x2d, weight_perm, module.bias, keep=keep, wmask=wm, residual=residual)
+        self.update_time_layer()
+        return y
 
     def hook_modules(self, model):
         if self.hook_module == 'text':
@@ -93,10 +126,8 @@ class WandaRemoveNeuronsFast(NeuronPredictivity):
     def linear_hook_fn(self, module, input, output):
         x = input[0]
         bits = self.device_bits(self.timestep, self.layer, module.weight.device)
-        if bits.shape[0] != module.weight.shape[0] or bits.shape[1] * 8 != module.weight.shape[1]:
-            raise ValueError(f"mask ({self.timestep},{self.layer}) shape {tuple(bits.shape)} does not match weight "
-                             f"{tuple(module.weight.shape)}")
-        y = module.run(x.reshape(-1, x.shape[-1]), wmask_bits=bits)
+        self._check_shape(bits, module.weight, "ff.net.2")
+        y = module.run(x.reshape(-1, x.shape[-1]), wmask=self.device_kmajor(self.timestep, self.layer, bits.device))
         self.update_time_layer()
         return y.view(*x.shape[:-1], module.weight.shape[0])
 
@@ -106,10 +137,8 @@ class WandaRemoveNeuronsFast(NeuronPredictivity):
         x = input[0]
         fc2 = module.fc2
         bits = self.device_bits(0, self.layer, fc2.weight.device)
-        if bits.shape[0] != fc2.weight.shape[0] or bits.shape[1] * 8 != fc2.weight.shape[1]:
-            raise ValueError(f"text mask (0,{self.layer}) shape {tuple(bits.shape)} does not match fc2 weight "
-                             f"{tuple(fc2.weight.shape)}")
-        y = module.run(x.reshape(-1, x.shape[-1]), wmask_bits=bits)
+        self._check_shape(bits, fc2.weight, "text fc2")
+        y = module.run(x.reshape(-1, x.shape[-1]), wmask=self.device_kmajor(0, self.layer, bits.device))
         self.update_time_layer()
         return y.view(*x.shape[:-1], fc2.weight.shape[0])
 
@@ -118,12 +147,12 @@ class WandaRemoveNeuronsFast(NeuronPredictivity):
         bits = self.device_bits(self.timestep, self.layer, module.proj.weight.device)
         key = ("gate_full", self.timestep, self.layer)
         full = self._dev.get(key)
-        if full is None:
+        if full is None:  # [value rows unmasked ; gate rows masked] in the masked GEMM's layout, once per (t, l)
             F4, Kb = bits.shape
             full = torch.cat([torch.zeros((F4, Kb), dtype=torch.uint8, device=bits.device), bits], 0).contiguous()
-            self._dev[key] = full
+            full = self._dev[key] = ops.wmask_kmajor(full)
         x = input[0]
-        y = module.proj.run(x.reshape(-1, x.shape[-1]), wmask_bits=full)
+        y = module.proj.run(x.reshape(-1, x.shape[-1]), wmask=full)
         gate = torch.empty((y.shape[0], module.inner_dim), dtype=torch.float16, device=y.device) \
             if self.store_gates else None
         from sdmoe.unet import act_code

@@ -141,8 +141,8 @@ class CLIPMLP(nn.Module):
         """act(fc1(x)) [rows, F] (one GEMM, activation in the epilogue)."""
         return self.fc1.run(x2d, act=self.activation_fn.code)
 
-    def run(self, x2d, residual=None, out=None, wmask_bits=None):
-        return self.fc2.run(self.hidden(x2d), residual=residual, out=out, wmask_bits=wmask_bits)
+    def run(self, x2d, residual=None, out=None, wmask=None):
+        return self.fc2.run(self.hidden(x2d), residual=residual, out=out, wmask=wmask)
 
     def forward(self, hidden_states):
         if self._sdmoe_deferred and self._forward_hooks:

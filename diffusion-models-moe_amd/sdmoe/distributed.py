@@ -23,6 +23,21 @@ def shard(prompts, rank, world_size):
     return list(prompts[lo:hi]), lo
 
 
+def run_shard(pipe, receiver, prompts, rank=None, world_size=None):
+    """This rank's part of a data-parallel batch: its contiguous shard of the GLOBAL prompt list, seeded at its
+    global offset (pipe.prompt_offset), through the receiver's observe_activation (the reference call shape,
+    base_receiver.py:40-77). Returns (outputs, offset)."""
+    ws, rk = world()
+    rank = rk if rank is None else rank
+    world_size = ws if world_size is None else world_size
+    mine, offset = shard(prompts, rank, world_size)
+    pipe.prompt_offset = offset
+    if hasattr(receiver, "reset_time_layer"):
+        receiver.reset_time_layer()
+    out, _ = receiver.observe_activation(pipe, mine)
+    return out, offset
+
+
 def broadcast_object(obj, src=0):
     """Python object (e.g. RemoveExperts lists {t: {l: [ids]}}) from `src` to every rank."""
     ws, rank = world()

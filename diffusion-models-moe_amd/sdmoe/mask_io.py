@@ -59,6 +59,25 @@ def unpack_mask(bits, cols) -> np.ndarray:
     return np.unpackbits(np.asarray(bits, dtype=np.uint8), axis=-1, count=cols, bitorder="little").astype(np.int64)
 
 
+def load_labels(path) -> list:
+    """Expert labels written by ParamSplit.save (moe_utils.py:54-61: torch.save([x for x in kmeans.labels_])), i.e.
+    a list of numpy int32/int64 scalars, or of Python ints. torch.load(weights_only=True) with only numpy's
+    scalar reconstructor and integer dtypes added to its allow-list: nothing else in the file can execute."""
+    import torch
+    core = getattr(np, "_core", None) or np.core
+    allowed = [core.multiarray.scalar, np.dtype]
+    for name in ("Int8DType", "Int16DType", "Int32DType", "Int64DType", "UInt8DType", "UInt16DType", "UInt32DType",
+                 "UInt64DType", "LongDType", "ULongDType", "LongLongDType", "ULongLongDType"):
+        t = getattr(np.dtypes, name, None)
+        if t is not None:
+            allowed.append(t)
+    with torch.serialization.safe_globals(allowed):
+        obj = torch.load(path, weights_only=True)
+    if isinstance(obj, torch.Tensor):
+        return obj.to(torch.int64).tolist()
+    return [int(v) for v in obj]
+
+
 def load_expert_list(path) -> list:
     with open(path) as f:
         return [int(e) for e in json.load(f)]

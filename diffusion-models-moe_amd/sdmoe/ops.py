@@ -97,16 +97,69 @@ def mask_weight(w, bits, out=None):
     return out
 
 
+def wmask_kmajor(bits, perm=None, out=None):
+    """Packed Wanda bits [N, K/8] (bit set = weight removed) -> the masked GEMM's K-step-major layout int64
+    [K/64, N] (sdmoe_wmask_kmajor); perm (int32 [K], optional): column j of the result = column perm[j] of the
+    mask (the routed FFN's expert-major neuron order). Made once per (t, l) mask, not per call."""
+    lib = _lib.load()
+    if bits.dim() != 2 or bits.dtype != torch.uint8:
+        raise ValueError(f"wmask bits must be uint8 [N, K/8], got {bits.dtype} {tuple(bits.shape)}")
+    N, K = bits.shape[0], bits.shape[1] * 8
+    if out is None:
+        out = torch.empty((K // 64, N), dtype=torch.int64, device=bits.device)
+    pp = None
+    if perm is not None:
+        if perm.dtype != torch.int32 or perm.numel() != K:
+            raise ValueError("perm must be int32 [K]")
+        pp = _dev(perm, "perm", torch.int32)
+    st = lib.sdmoe_wmask_kmajor(_dev(bits, "bits", torch.uint8), bits.stride(0), N, K, pp,
+                                _dev(out, "out", torch.int64), _stream())
+    _lib.check(st, "sdmoe_wmask_kmajor")
+    return out
+
+
+def linear_masked(x, w, bias=None, *, keep=None, wmask=None, residual=None, out=None):
+    """out = (x ⊙ keep) @ (w ⊙ (1 - M))^T + bias + residual (sdmoe_linear_masked): keep int64 [K/64, M] (A keep bits,
+    sdmoe_moe_topk_keep), wmask int64 [K/64, N] (wmask_kmajor). Either may be None."""
+    lib = _lib.load()
+    xp, lda = _rows(x, "x")
+    M, K = x.shape
+    N = w.shape[0]
+    if w.shape[1] != K:
+        raise ValueError(f"linear_masked: weight {tuple(w.shape)} does not match input K={K}")
+    if keep is not None and (tuple(keep.shape) != (K // 64, M) or keep.dtype != torch.int64):
+        raise ValueError(f"keep must be int64 [{K // 64}, {M}], got {keep.dtype} {tuple(keep.shape)}")
+    if wmask is not None and (tuple(wmask.shape) != (K // 64, N) or wmask.dtype != torch.int64):
+        raise ValueError(f"wmask must be int64 [{K // 64}, {N}], got {wmask.dtype} {tuple(wmask.shape)}")
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float16, device=x.device)
+    op, ldc = _rows(out, "out")
+    rp, ldr = (None, 0) if residual is None else _rows(residual, "residual")
+    ws = _workspace(x.device)
+    st = lib.sdmoe_linear_masked(xp, lda, None if keep is None else _dev(keep, "keep", torch.int64), _dev(w, "w"),
+                                 w.stride(0), None if wmask is None else _dev(wmask, "wmask", torch.int64),
+                                 _ptr(bias), rp, ldr, op, ldc, M, N, K, ws.data_ptr(), ws.numel(), _stream())
+    _lib.check(st, "sdmoe_linear_masked")
+    return out
+
+
 def linear(x, w, bias=None, *, out=None, residual=None, act=ACT_NONE, coladd=None, coladd_bstride=0,
-           rows_per_batch=0, gn=None, wmask_bits=None):
+           rows_per_batch=0, gn=None, wmask=None, wmask_bits=None):
     """out = act(GN?(x) @ w.T + bias + coladd) + residual.  w: [N, K] fp16 (nn.Linear layout).
     gn = (scale, shift, silu): per-(image, channel) GroupNorm apply on x first (rows_per_batch rows/image).
-    wmask_bits: Wanda bitmask [N, K/8] zeroing weights (remove_wanda_neurons_fast.py:69-83)."""
+    wmask: Wanda mask in the GEMM's layout (wmask_kmajor) applied to the W fragments in the GEMM
+    (remove_wanda_neurons_fast.py:69-83); wmask_bits: the same mask packed [N, K/8], converted on this call."""
     lib = _lib.load()
     if gn is not None:
         x = groupnorm_apply(x, x.shape[0] // rows_per_batch, rows_per_batch, gn[0], gn[1], gn[2])
     if wmask_bits is not None:
-        w = mask_weight(w, wmask_bits)
+        if tuple(wmask_bits.shape) != (w.shape[0], w.shape[1] // 8):
+            raise ValueError(f"mask bits {tuple(wmask_bits.shape)} do not match weight {tuple(w.shape)}")
+        wmask = wmask_kmajor(wmask_bits)
+    if wmask is not None:
+        if act != ACT_NONE or coladd is not None:
+            raise ValueError("linear: a Wanda weight mask combines with bias/residual only")
+        return linear_masked(x, w, bias, wmask=wmask, residual=residual, out=out)
     xp, lda = _rows(x, "x")
     M, K = x.shape
     N = w.shape[0]
@@ -246,6 +299,7 @@ class Routing:
         sizes = set(counts.tolist())
         self.esize = sizes.pop() if len(sizes) == 1 else 0
         self.perm = order  # new neuron position -> original neuron id (cpu int64)
+        self.perm_dev = order.to(torch.int32).to(device)  # the same on the device (Wanda mask column permutation)
         self.fusable = bool(self.esize and 40 % self.esize == 0 and F % 80 == 0 and self.E <= 256)
 
     @classmethod
@@ -318,8 +372,11 @@ def moe_topk_keep(score, routing: "Routing", M: int, removed=None, sel_out=None,
     return keep
 
 
-def linear_keep(x, keep, w, bias=None, *, residual=None, out=None):
-    """out = (x with the neurons whose keep bit is clear zeroed) @ w.T + bias + residual (sdmoe_linear_keep)."""
+def linear_keep(x, keep, w, bias=None, *, residual=None, out=None, wmask=None):
+    """out = (x with the neurons whose keep bit is clear zeroed) @ w.T + bias + residual (sdmoe_linear_keep);
+    with wmask (wmask_kmajor layout) the Wanda weight mask too (sdmoe_linear_masked)."""
+    if wmask is not None:
+        return linear_masked(x, w, bias, keep=keep, wmask=wmask, residual=residual, out=out)
     lib = _lib.load()
     xp, lda = _rows(x, "x")
     M, K = x.shape

@@ -232,6 +232,17 @@ class GEGLU(nn.Module):
         return self.routed(x)[0]
 
 
+def _sole_receiver(module, method):
+    """The sdmoe receiver owning `module`'s only forward hook, if it has `method`; else None."""
+    hooks = list(module._forward_hooks.values())
+    if len(hooks) != 1:
+        return None
+    owner = getattr(hooks[0], "__self__", None)
+    if owner is None or not getattr(owner, "_sdmoe_receiver", False) or not hasattr(owner, method):
+        return None
+    return owner
+
+
 class FeedForward(nn.Module):
     def __init__(self, geglu, down):
         super().__init__()
@@ -248,23 +259,36 @@ class FeedForward(nn.Module):
         return self._wperm
 
     def run(self, x2d, nimg, residual):
+        """GEGLU -> down projection (+ the block's residual). The fused routed GEGLU (GEGLU.routed) hands over an
+        expert-permuted product whose top-k mask is still pending (applied by the down projection as it reads it);
+        that intermediate must stay private to this FeedForward, so the fused path runs only when
+          * the GEGLU has no forward hook, or exactly one owned by an sdmoe receiver (whose hook_fn computes it), and
+          * ff.net.2 has no hook, or exactly one owned by a receiver that can apply its weight mask in the fused form
+            (WandaRemoveNeuronsFast.fused_linear: same (t, l) mask, columns permuted, counter advanced).
+        Any other hook sees exactly the reference's tensors (natural neuron order, mask applied)."""
         geglu, down = self.net[0], self.net[2]
-        # a hook on the down projection (Wanda weight masks) sees the natural neuron order
-        geglu._allow_permuted_out = not down._forward_hooks
+        dhooks = bool(down._forward_hooks)
+        masker = _sole_receiver(down, "fused_linear") if dhooks else None
+        geglu._allow_permuted_out = (not dhooks or masker is not None) and (
+            not geglu._forward_hooks or _sole_receiver(geglu, "hook_fn") is not None)
         try:
             h = geglu(x2d.view(nimg, -1, x2d.shape[1]))
         finally:
             geglu._allow_permuted_out = False
-        if down._forward_hooks:
-            o = down(h)
-            return ops.add(o.reshape(residual.shape).contiguous(), residual)
         h2 = h.reshape(-1, h.shape[-1])
         perm = geglu._out_perm
-        if perm is not None and perm[1] == h2.data_ptr():
+        permuted = perm is not None and perm[1] == h2.data_ptr()
+        if dhooks and not (permuted and masker is not None):
+            o = down(h)  # the hook sees the natural neuron order
+            return ops.add(o.reshape(residual.shape).contiguous(), residual)
+        if permuted:
             wp = self._down_weight_permuted(perm[0])
             keep = geglu._out_keep
-            if keep is not None and keep[1] == h2.data_ptr():
-                return ops.linear_keep(h2, keep[0], wp, down.bias, residual=residual)
+            keep = keep[0] if keep is not None and keep[1] == h2.data_ptr() else None
+            if masker is not None:
+                return masker.fused_linear(down, h2, keep, perm[0].perm_dev, wp, residual)
+            if keep is not None:
+                return ops.linear_keep(h2, keep, wp, down.bias, residual=residual)
             return ops.linear(h2, wp, down.bias, residual=residual)
         return down.run(h2, residual=residual)
 

@@ -153,6 +153,30 @@ int sdmoe_linear_keep(const void* A, long lda, const void* keep, const void* W, 
                       long workspace_floats, void* stream);
 
 /*
+ * sdmoe_linear_masked — SURVEY §8b's masked linear: C = (A ⊙ keep) @ (W ⊙ (1 - M))^T + bias + R with both masks
+ * applied to the MFMA fragments after their LDS read (no masked copy of A or W is ever written):
+ *   keep  (nullable): the A operand's per-(row, k) keep bits, layout of sdmoe_moe_topk_keep ([K/64][M] 64-bit words);
+ *   wmask (nullable): the Wanda weight mask in the same K-step-major layout over W's rows ([K/64][N] 64-bit words,
+ *     bit j of word (s, n) SET = W[n, 64 s + j] removed), made once per mask by sdmoe_wmask_kmajor.
+ * Both NULL = sdmoe_linear without coladd/act. K % 64 == 0, N % 8 == 0, strides % 8 == 0.
+ * Replaces: F.linear(input[0], W.clone() * (1 - M[t][l]), b) of WandaRemoveNeuronsFast.linear_hook_fn
+ * (neuron_receivers/remove_wanda_neurons_fast.py:69-83) -- no W clone, no mask H2D copy, no second GEMM -- and,
+ * with keep, that hook under MoE routing (the union remover of multi_concept_remover.py:43-53 on a MoE-fied U-Net,
+ * BASELINE config 4).
+ */
+int sdmoe_linear_masked(const void* A, long lda, const void* keep, const void* W, long ldw, const void* wmask,
+                        const void* bias, const void* R, long ldr, void* C, long ldc, int M, int N, int K,
+                        float* workspace, long workspace_floats, void* stream);
+
+/*
+ * sdmoe_wmask_kmajor — packed Wanda bits [N][K/8] (row stride ldb bytes; bit k%8 of byte (n, k/8) = W[n, k] removed;
+ * the layout of the reference's [C, 4C] masks bit-packed, sdmoe/mask_io.py) -> out [K/64][N] 64-bit words for
+ * sdmoe_linear_masked. perm (nullable, int32 [K]) permutes the columns: bit j of word (s, n) = mask(n, perm[64 s + j])
+ * -- the FFN down projection's expert-major neuron order of the fused routed path. K % 64 == 0.
+ */
+int sdmoe_wmask_kmajor(const void* bits, long ldb, int N, int K, const int* perm, void* out, void* stream);
+
+/*
  * Skill discovery on the same hook seam.
  * sdmoe_expert_mean_topk — GetExperts.hook_fn (neuron_receivers/get_experts.py:50-83): mean over tokens of the
  *   fp16 expert scores [M, E] (score_within_bb.mean(0): fp32 accumulate, one rounding to fp16), restricted to the

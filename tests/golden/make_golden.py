@@ -14,7 +14,7 @@ Covered reference functions:
   * GetExperts.hook_fn                   neuron_receivers/get_experts.py:50-83 (token-mean expert top-k, bboxes)
   * Wanda.hook_fn + TimeLayerColumnNorm  neuron_receivers/wanda_receiver.py:37-57, utils.py:321-370
 
-usage: PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+usage: PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [name-prefix ...]
 """
 from __future__ import annotations
 
@@ -188,6 +188,8 @@ def gen_remove_experts(helper, rem_mod):
         (320, 32, "gelu", -1.5, torch.float16),  # mostly negative expert scores: removed experts (score 0) win slots
         (640, 16, "relu", 0.0, torch.float16),
         (320, 32, "gelu", -1.5, torch.float32),
+        (1280, 8, "relu", 0.0, torch.float16),   # E = 256, k = 51 (the 16x16 / 8x8 levels)
+        (1280, 8, "gelu", -1.0, torch.float16),
     ]
     for i, (C, N, act, gb, dtype) in enumerate(spec):
         seed = 2000 + i
@@ -337,9 +339,16 @@ def gen_wanda_receiver(w_mod):
     return cases
 
 
-def save(cases):
+def save(cases, only=None):
+    """Write the cases (only those whose name starts with one of `only`, if given) and merge index.json."""
     index = []
+    ipath = os.path.join(OUT, "index.json")
+    if only and os.path.exists(ipath):
+        with open(ipath) as f:
+            index = list(json.load(f)["cases"])
     for c in cases:
+        if only and not any(c["name"].startswith(o) for o in only):
+            continue
         name = c.pop("name")
         arrays = {}
         for k, v in c.items():
@@ -348,7 +357,8 @@ def save(cases):
             else:
                 arrays[k] = np.array(v)
         np.savez_compressed(os.path.join(OUT, name + ".npz"), **arrays)
-        index.append(name)
+        if name not in index:
+            index.append(name)
     with open(os.path.join(OUT, "index.json"), "w") as f:
         json.dump({"cases": index, "generator": "tests/golden/make_golden.py", "reference": "ruchikachavhan/"
                    "diffusion-models-moe @ 2024-10-08", "torch": torch.__version__}, f, indent=1)
@@ -367,8 +377,9 @@ def main():
     wr = load_ref("neuron_receivers.wanda_receiver", "neuron_receivers/wanda_receiver.py")
     cases = gen_moefy(helper, moefy) + gen_remove_experts(helper, rem) + gen_wanda(wanda) + gen_counter(pred)
     cases += gen_get_experts(helper, ge) + gen_wanda_receiver(wr)
-    save(cases)
-    print(f"wrote {len(cases)} golden cases to {OUT}")
+    only = sys.argv[1:] or None  # optional name prefixes: regenerate just those fixtures
+    save(cases, only)
+    print(f"wrote {'all' if only is None else only} golden cases to {OUT}")
 
 
 if __name__ == "__main__":

@@ -264,3 +264,106 @@ def test_cfg_ddim_step_and_prepare():
     ref = math.sqrt(a_p) * x0 + math.sqrt(1 - a_p) * ee
     ops.cfg_ddim_step(eps, lat, True, g, a_t, a_p, next_in=x_in)
     close(lat, ref, tol=1e-4)
+
+
+# ---- the bench workload's exact shapes (SD-1.4 512^2, U-Net batch 16: 64x64 latents = 65,536 rows) ----------
+
+@pytest.mark.parametrize("d,N", [(40, 4096), (64, 4096)])
+def test_attention_full_size(d, N):
+    """Self-attention at the metric's N = 4096 tokens (d = 40: SD-1.4 64x64 level; d = 64: SDXL-base), 8 heads,
+    2 images (the kernel's grid is per (image, head), so more images only repeat these blocks)."""
+    nimg, heads = 2, 8
+    C = heads * d
+    qkv = rnd(nimg * N, 3 * C, seed=50 + d)
+    q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
+    out = ops.attention(q, k, v, nimg, N, N, heads)
+    qf = q.float().reshape(nimg, N, heads, d).transpose(1, 2)
+    kf = k.float().reshape(nimg, N, heads, d).transpose(1, 2)
+    vf = v.float().reshape(nimg, N, heads, d).transpose(1, 2)
+    ref = F.scaled_dot_product_attention(qf, kf, vf).transpose(1, 2).reshape(nimg * N, C)
+    close(out, ref)
+
+
+def _with_tune(settings, fn):
+    from sdmoe import _lib
+    lib = _lib.load()
+    try:
+        for knob, val in settings:
+            _lib.check(lib.sdmoe_tune(knob, val), "tune")
+        fn()
+    finally:
+        _lib.check(lib.sdmoe_tune(0, 0), "tune")
+        _lib.check(lib.sdmoe_tune(1, 0), "tune")
+
+
+# tiles (sdmoe_tune knob 1): 0 auto, 1 = 128x160, 2 = 64x160, 3 = 256x320 (2x4 waves), 4 = 256x160 (4x2), 5 = 256x320
+# (4x2); stages (knob 0): 0 auto, 2, 3 -- every ring the M = 65,536 problems can take
+FULL_TILES = [(t, s) for t in (0, 1, 2, 3, 4, 5) for s in (0, 2, 3)]
+
+
+@pytest.mark.parametrize("tile,stages", FULL_TILES)
+def test_linear_full_size_tiles(tile, stages):
+    """The 25 per-evaluation [65536, 320] x [320, 320] projections (+bias +residual) on every tile / stage ring."""
+    M, N, K = 65536, 320, 320
+    x, w = rnd(M, K, seed=60), rnd(N, K, scale=K ** -0.5, seed=61)
+    b, r = rnd(N, scale=0.1, seed=62), rnd(M, N, seed=63)
+
+    def run():
+        close(ops.linear(x, w, b, residual=r), x.float() @ w.float().t() + b.float() + r.float())
+    _with_tune([(1, tile), (0, stages)], run)
+
+
+@pytest.mark.parametrize("tile,stages", FULL_TILES)
+def test_conv3x3_full_size_tiles(tile, stages):
+    """The 64x64 320->320 ResNet conv at U-Net batch 16 (M = 65,536, K = 2,880) with the time-embedding column
+    add and residual epilogue, on every tile / stage ring."""
+    nimg, H, C = 16, 64, 320
+    x = rnd(nimg * H * H, C, seed=64)
+    w, b = rnd(C, 3, 3, C, scale=(9 * C) ** -0.5, seed=65), rnd(C, scale=0.1, seed=66)
+    temb, res = rnd(1, C, seed=67), rnd(nimg * H * H, C, seed=68)
+
+    def run():
+        out = ops.conv3x3(x, nimg, H, H, w, b, coladd=temb, coladd_bstride=0, residual=res)
+        close(out, conv_ref(x, nimg, H, H, w, b) + temb.float() + res.float())
+    _with_tune([(1, tile), (0, stages)], run)
+
+
+def test_conv3x3_full_size_upsample_concat():
+    """The 32x32 -> 64x64 upsample conv (640 ch) and a 64x64 skip-concat conv input (960 -> 320) at batch 16."""
+    nimg = 16
+    x = rnd(nimg * 32 * 32, 640, seed=69)
+    w, b = rnd(640, 3, 3, 640, scale=(9 * 640) ** -0.5, seed=70), rnd(640, scale=0.1, seed=71)
+    close(ops.conv3x3(x, nimg, 32, 32, w, b, upsample=True), conv_ref(x, nimg, 32, 32, w, b, 1, True))
+    buf = rnd(nimg * 64 * 64, 960, seed=72)
+    w2 = rnd(320, 3, 3, 960, scale=(9 * 960) ** -0.5, seed=73)
+    close(ops.conv3x3(buf, nimg, 64, 64, w2, b[:320]), conv_ref(buf, nimg, 64, 64, w2, b[:320]))
+
+
+@pytest.mark.parametrize("C,HW", [(320, 4096), (640, 4096), (960, 4096)])
+def test_groupnorm_full_size(C, HW):
+    """GroupNorm(32) statistics + apply(+SiLU) at the bench's 16 images x 4096 positions (the partial/finalize path)."""
+    nimg = 16
+    x = rnd(nimg * HW, C, seed=74) * 2 + 1
+    gamma, beta = rnd(C, scale=0.1, seed=75) + 1, rnd(C, scale=0.1, seed=76)
+    y = ops.groupnorm(x, nimg, HW, gamma, beta, 1e-5, 32, True)
+    ref = F.group_norm(x.float().reshape(nimg, HW, C).permute(0, 2, 1), 32, gamma.float(), beta.float(), 1e-5)
+    close(y, F.silu(ref.permute(0, 2, 1).reshape(nimg * HW, C)), tol=5e-3)
+
+
+def test_geglu_fused_full_size():
+    """The 64x64 level's fused projection + ReLU GEGLU + expert scores at M = 65,536 (F = 1280, 64 experts of 20)
+    against the unfused projection GEMM + route kernel: bit-identical."""
+    M, C, E = 65536, 320, 64
+    F_ = 4 * C
+    g = torch.Generator().manual_seed(77)
+    x = torch.randn(M, C, generator=g).half().to(DEV)
+    w = (torch.randn(2 * F_, C, generator=g) * C ** -0.5).half().to(DEV)
+    b = (torch.randn(2 * F_, generator=g) * 0.3).half().to(DEV)
+    routing = ops.Routing(torch.randperm(F_, generator=g) % E, E, 12, DEV)
+    w_il, b_il = ops.interleave_geglu(w, b, routing.perm)
+    score = torch.empty((M, E), dtype=torch.float16, device=DEV)
+    P = ops.linear_geglu(x, w_il, b_il, ops.ACT_RELU, score=score, esize=routing.esize)
+    score_u = torch.empty_like(score)
+    out_u = ops.geglu_route(ops.linear(x, w, b), routing, ops.ACT_RELU, score_out=score_u, k=E)
+    assert torch.equal(score, score_u)
+    assert torch.equal(P, out_u[:, routing.perm.to(DEV)])

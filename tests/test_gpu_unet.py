@@ -406,3 +406,49 @@ def test_pipeline_pndm_remove_experts_tiny(tiny):
                      ff_hook_factory=forced_factory(layers, "gelu", rec.sels, lists, stats))
     assert stats["clear_mismatch"] == 0, stats
     assert rel_l2(out[0], exp[0]) <= 1e-2
+
+
+def test_pipeline_metric_workload_sd14_64x64(parity_report):
+    """The bench's workload at 2 DDIM steps: SD-1.4 at 64x64 latents (512^2), 2 prompts (U-Net batch 4 with CFG),
+    relufied, MoE-fied (expert 20, top-k 0.2), RemoveExperts with removal active (t < 20) through
+    observe_activation on the fused + keep path (sdmoe_linear_geglu -> sdmoe_moe_topk_keep -> sdmoe_linear_keep),
+    against the fp32 oracle with the reference hook in fp16 (remove_skilled_experts.py:24-55).
+    Contract: the device's top-k selection equals the oracle's on every row whose k-th/(k+1)-th fp16 score gap is
+    clear of near-tie noise (16 ulps: the two trunks' fp16 vs fp32 activations feed the hook); near-tie rows are
+    teacher-forced and counted; final latents rel L2 <= 1e-2."""
+    from moefication.helper import moefy_synthetic
+    from sparsity.relufy_model import find_and_change_geglu
+    from neuron_receivers import GEGLU, RemoveExperts
+    import sdmoe.unet as U
+    assert U.FUSED_GEGLU and U.FUSED_KEEP
+    cfg = UNetConfig.sd14(64)
+    sd = make_state_dict(cfg, 11)
+    unet = UNet2DConditionModel.from_state_dict(sd, cfg, DEV)
+    pipe = StableDiffusionPipeline(unet, DEV, num_inference_steps=2)
+    find_and_change_geglu(pipe.unet)
+    moefy_synthetic(pipe, 0.2, 20, seed=12)
+    mods = [m for n, m in pipe.unet.named_modules() if n.endswith("ff.net.0")]
+    layers = [(m.labels.numpy(), m.patterns.shape[0], m.k) for m in mods]
+    assert [k for _, _, k in layers] == [12, 12, 25, 25, 51, 51, 51, 51, 51, 51, 25, 25, 25, 12, 12, 12]
+    g = torch.Generator().manual_seed(13)
+    T, L = 2, 16
+    lists = {t: {l: sorted(torch.randperm(layers[l][1], generator=g)[:layers[l][1] // 10].tolist())
+                 for l in range(L)} for t in range(T)}
+    rec = recording(RemoveExperts)(0, None, T, L, replace_fn=GEGLU, expert_indices=lists, store_gates=False)
+    rec.sels = []
+    prompts = ["Starry night by Van Gogh", "a wheat field with cypresses"]
+    out, _ = rec.observe_activation(pipe, prompts)
+    torch.cuda.synchronize()
+    assert (rec.timestep, rec.layer) == (2, 0) and len(rec.sels) == T * L
+    assert all(m._out_keep is not None for m in mods), "fused + keep path did not run"
+    got = torch.stack(out).float().cpu()
+    del unet, pipe
+    torch.cuda.empty_cache()
+    ref = UNetRef({k: v.half().float() for k, v in sd.items()}, cfg)
+    stats = dict(rows=0, clear=0, clear_mismatch=0, forced=0)
+    exp = run_oracle(ref, cfg, prompts, 2, ff_hook_factory=forced_factory(layers, "relu", rec.sels, lists, stats))
+    parity_report("pipeline_sd14_64x64_remove_relu_topk0.2", rows=stats["rows"], clear=stats["clear"],
+                  near_tie=stats["rows"] - stats["clear"], flips=stats["forced"], rel_l2=rel_l2(got, exp))
+    assert stats["clear_mismatch"] == 0, stats
+    assert torch.isfinite(got).all()
+    assert rel_l2(got, exp) <= 1e-2

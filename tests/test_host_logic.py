@@ -121,6 +121,71 @@ def test_union_of_packed_masks_equals_oracle_or():
     assert mc.union_neuron_remover.dense_mask(0, 0).sum() == 0
 
 
+def test_union_starts_from_last_concept_and_accumulates():
+    """multi_concept_remover.py:24-33: the union remover is built from the last configured concept's masks, and
+    handle_multiple_concepts ORs into it (:43-53) until reset_union_remover (:35-41)."""
+    from oracle import hooks_ref as H
+    from neuron_receivers import WandaRemoveNeuronsFast, MultiConceptRemoverWanda
+    rng = np.random.default_rng(5)
+    T, L = 1, 2
+    concepts = {c: {t: {l: (rng.random((16, 64)) < 0.1).astype(np.int64) for l in range(L)} for t in range(T)}
+                for c in ("a", "b", "c")}
+    removers = {c: WandaRemoveNeuronsFast(0, None, T, L, masks=m) for c, m in concepts.items()}
+    mc = MultiConceptRemoverWanda(None, 0, T, L, concepts_to_remove=list(concepts), removers=removers)
+    assert np.array_equal(mc.union_neuron_remover.dense_mask(0, 1), concepts["c"][0][1])
+    mc.handle_multiple_concepts(["a", "b"])
+    exp = H.union_masks([concepts[c][0][1] for c in ("a", "b", "c")])
+    assert np.array_equal(mc.union_neuron_remover.dense_mask(0, 1), exp)
+
+
+def test_remove_concepts_two_value_contract():
+    """unified_editing.py:126 unpacks `output, single_image_removal = remove_concepts(...)` for 0, 1 and several
+    concepts; output is [original | removed] side by side (multi_concept_remover.py:83-99)."""
+    from neuron_receivers import WandaRemoveNeuronsFast, MultiConceptRemoverWanda
+    T, L = 1, 1
+    removers = {c: WandaRemoveNeuronsFast(0, None, T, L, masks={0: {0: np.zeros((8, 16), np.int64)}})
+                for c in ("x", "y")}
+    mc = MultiConceptRemoverWanda(None, 0, T, L, concepts_to_remove=["x", "y"], removers=removers)
+    calls = []
+
+    class FakePipe:
+        def __call__(self, prompt, **kw):
+            calls.append(prompt)
+            return type("O", (), {"images": [torch.full((4, 8, 8), float(len(calls)))]})()
+    for r in removers.values():  # no GPU here: the receivers' pipeline call is the fake one
+        r.observe_activation = lambda model, ann, bboxes=None: (model(ann).images[0], [])
+    mc.union_neuron_remover.observe_activation = lambda model, ann, bboxes=None: (model(ann).images[0], [])
+    out, singles = mc.remove_concepts(FakePipe(), "p", [])
+    assert singles is None and tuple(out.shape) == (4, 8, 8)
+    out, singles = mc.remove_concepts(FakePipe(), "p", ["x"])
+    assert singles is None and tuple(out.shape) == (4, 8, 16)
+    assert torch.equal(out[..., 8:], mc.last_outputs["removal"]) and torch.equal(out[..., :8],
+                                                                                  mc.last_outputs["original"])
+    out, singles = mc.remove_concepts(FakePipe(), "p", ["x", "y"])
+    assert tuple(out.shape) == (4, 8, 16) and len(singles) == 2 and tuple(singles[0].shape) == (4, 8, 16)
+
+
+def test_modify_ffn_reads_numpy_scalar_labels(tmp_path):
+    """ParamSplit.save writes [x for x in kmeans.labels_] -- numpy int32 scalars (moe_utils.py:54-61): they load
+    through the restricted weights_only path; a file with any other global is refused."""
+    from moefication.helper import modify_ffn, balanced_random_labels
+    from sdmoe import mask_io
+    from sdmoe.unet import GEGLU, LoRACompatibleLinear
+    lab = balanced_random_labels(1280, 20, 2)
+    for dt in (np.int32, np.int64):
+        g = GEGLU(LoRACompatibleLinear(torch.zeros(2 * 1280, 320, dtype=torch.float16)))
+        torch.save([dt(v) for v in lab], tmp_path / "labels")
+        modify_ffn(g, str(tmp_path / "labels"), 0.2)
+        assert g.k == 12 and torch.equal(g.patterns.float().argmax(0), torch.from_numpy(lab))
+
+    class Evil:
+        def __reduce__(self):
+            return (print, ("pwned",))
+    torch.save([Evil()], tmp_path / "evil")
+    with pytest.raises(Exception):
+        mask_io.load_labels(str(tmp_path / "evil"))
+
+
 def test_union_random_drop_is_seeded_and_subset():
     from oracle import hooks_ref as H
     rng = np.random.default_rng(4)

@@ -1,6 +1,11 @@
-# run GPU tests matching $1 (pytest -k expression; default all)
-set -eu
+#!/bin/bash
+# Full -m gpu suite on the GPU box (stop at the first failure), with the near-tie/flip parity report.
+# usage: gpurun -- bash tools/gpu_tests.sh [pytest selection args]
+set -u
 mkdir -p gpurun_out
-K=${1:-}
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${K:+-k "$K"} > gpurun_out/t.log 2>&1 || { tail -60 gpurun_out/t.log; exit 1; }
-grep -E "PASS|FAIL|passed|failed" gpurun_out/t.log | tail -40
+export SDMOE_PARITY_REPORT=gpurun_out/parity_report.json
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread "$@" \
+  > gpurun_out/gputests.log 2>&1
+rc=$?
+tail -25 gpurun_out/gputests.log
+exit $rc
