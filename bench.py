@@ -336,13 +336,18 @@ def main():
         n, ms, flops = timer.result()
         if n:
             achieved = flops / (ms / 1e3) / 1e12
-            traffic = None
+            traffic, traffic_src = None, None
             if args.traffic and os.path.exists(args.traffic) and args.model == "sd14":  # PMC file is the SD-1.4 run
-                traffic = json.load(open(args.traffic)).get("bytes_per_launch")
+                pmc = json.load(open(args.traffic))
+                traffic = pmc.get("bytes_per_launch")
+                # not measured in this process: the committed rocprofv3 --pmc passes (FETCH_SIZE x2, WRITE_SIZE) of
+                # this bench command on the build named in the file
+                traffic_src = (f"{os.path.relpath(args.traffic, ROOT)} (rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes"
+                               f" of bench.py, build {pmc.get('build', '?')})")
             roof = {"bound": "mfma", "kernel": "sdmoe_conv3x3: implicit-GEMM conv (gemm_kernel<BM,BN,MODE=1|2,STAGES>"
                                                " + split-K reduce where used)",
                     "achieved": round(achieved, 1), "peak": PEAK_FP16_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(achieved / PEAK_FP16_TFLOPS, 4), "traffic": traffic,
+                    "frac": round(achieved / PEAK_FP16_TFLOPS, 4), "traffic": traffic, "traffic_source": traffic_src,
                     "launches": n, "avg_launch_ms": round(ms / n, 4),
                     "algorithmic_flop_per_launch": round(flops / n)}
     cpu = None

@@ -4,7 +4,8 @@
 //   * Linear layers (attention q/k/v/out, proj_in/proj_out 1x1 convs, GEGLU proj, FFN down-proj, time MLP):
 //     activations [M, K] row-major (any row stride), weights [N, K] (nn.Linear layout);
 //   * ResNet 3x3 convolutions (stride 1/2, fused nearest-2x upsample) on NHWC activations: weights
-//     [Cout][3][3][Cin] so K = 9*Cin is contiguous per output channel and every 64-wide K-step is one tap.
+//     [Cout][Cin/64][3][3][64] so K = 9*Cin is contiguous per output channel, every 64-wide K-step is one tap of
+//     one 64-channel slice, and the 9 taps of a slice are consecutive K-steps (L2 reuse of the activation rows).
 // Main loop: 256 threads = 2x2 waves, BK = 64, 16x16x32 f16 MFMA. Both operand tiles go HBM -> LDS with
 // global_load_lds_dwordx4 (LDS-DMA, no register staging), one 1-KiB wave-instruction per 8 rows; conv halo
 // rows and M/N tails point at a zero line. A 3-stage LDS ring keeps two K-steps in flight behind a counted
@@ -22,11 +23,20 @@ namespace {
 
 constexpr int BK = 64;
 
+// 1: software-pipelined MFMA fragment reads in the GEMM main loop (next A pair read before the current pair's MFMAs);
+// 0: all fragments of a 32-deep slice read, then its MFMAs (kept buildable for same-box A/B: make GEMM_PIPE=0)
+#ifndef SDMOE_GEMM_PIPE
+#define SDMOE_GEMM_PIPE 1
+#endif
+
 // tuning knobs (sdmoe_tune): 0 = LDS stages (0 = auto, 2 or 3); 1 = forced tile config (0 = auto)
 int g_stages = 0;
 int g_tile = 0;
 int g_bk = 0;
 int g_prio = 0;
+int g_diag = 0;  // knob 6, diagnostics only (results garbage): bit 0 = no K-loop operand loads, bit 1 = no MFMAs,
+                 // bit 2 = no epilogue (nothing stored)
+int g_sched = 0;  // knob 6, diagnostics only: bit 0 = no K-loop operand loads, bit 1 = no MFMAs (results garbage)
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
@@ -51,6 +61,7 @@ struct GemmParams {
   half_t* score; long ld_score;
   int esize;
   int prio;  // experiment knob: raise wave priority around the MFMA block
+  int diag;  // diagnostic knob (sdmoe_tune 6): bit 0 skips the K-loop loads, bit 1 the MFMAs
   // expert keep mask of the A operand (MODE_KEEP / MODE_KEEPW): keep[(k / 64) * M * 8 + m * 8 + (k % 64) / 8] bit
   // (k % 8) = neuron k of token m survives the top-k; the A fragments are ANDed with it after their LDS read
   const uint8_t* keep;
@@ -314,9 +325,10 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
   auto a_dst = [&](int j) { return (j * NW + wave < A_INS) ? (j * NW + wave) * 1024 : STAGE_AB; };
   auto b_dst = [&](int j) { return (j * NW + wave < B_INS) ? BM * BK * 2 + (j * NW + wave) * 1024 : STAGE_AB; };
 
-  // conv K walk: (tap, 64-channel step) advanced incrementally in scalar registers
-  const int csteps = CONV ? p.Cin / BK : 1;
-  int st_tap = CONV ? ks0 / csteps : 0, st_c = CONV ? ks0 - st_tap * csteps : 0;
+  // conv K walk: (64-channel step, tap) advanced incrementally in scalar registers. Channel-step-major: the 9
+  // consecutive K-steps of one 64-channel slice re-read the same activation rows (shifted by a tap), so a
+  // workgroup's A working set is ~(BM + halo) x 128 B and stays in the XCD's L2 across the taps.
+  int st_c = CONV ? ks0 / 9 : 0, st_tap = CONV ? ks0 - st_c * 9 : 0;
 
   auto issue_stage = [&](int ks, int buf) {
     char* sa = smem + buf * STAGE;
@@ -329,7 +341,7 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
       const int kh = tap >= 6 ? 2 : (tap >= 3 ? 1 : 0);
       const int kw = tap - 3 * kh;
       const int c0b = st_c * BK * 2;
-      if (++st_c == csteps) { st_c = 0; ++st_tap; }
+      if (++st_tap == 9) { st_tap = 0; ++st_c; }
       if (MODE == MODE_CONV) {
         const unsigned tapoff = (unsigned)(((kh - 1) * p.Wd + (kw - 1)) * (int)p.lda * 2 + c0b);
 #pragma unroll
@@ -381,44 +393,93 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
     }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (it + NSTAGE - 1 < nk) issue_stage(ks0 + it + NSTAGE - 1, (it + NSTAGE - 1) % NSTAGE);
+    if (it + NSTAGE - 1 < nk && !(p.diag & 1)) issue_stage(ks0 + it + NSTAGE - 1, (it + NSTAGE - 1) % NSTAGE);
 
     const char* sa = smem + (it % NSTAGE) * STAGE;
     const char* sbm = sa + BM * BK * 2;
     if (p.prio) __builtin_amdgcn_s_setprio(1);
+    if (p.diag & 2) continue;
+    // fragment reads (A masked by MoE keep bits, B by Wanda bits where the mode says so)
+    auto read_a = [&](int kk, int i) -> half8 {
+      const int row = wr * WM + i * 16 + fr;
+      half8 a = *reinterpret_cast<const half8*>(sa + row * RB + (((kk * 4 + fg) ^ swzk(row)) << 4));
+      if constexpr (AKEEP) {  // zero the neurons of this row's dropped experts (8 neurons = chunk kk*4+fg)
+        const unsigned kbyte = *reinterpret_cast<const unsigned char*>(sa + KEEP_OFF + row * 8 + kk * 4 + fg);
+        const uint2v lo = *reinterpret_cast<const uint2v*>(smem + LUT_OFF + (kbyte & 15u) * 8);
+        const uint2v hi = *reinterpret_cast<const uint2v*>(smem + LUT_OFF + (kbyte >> 4) * 8);
+        uint4v u = __builtin_bit_cast(uint4v, a);
+        u[0] &= lo[0]; u[1] &= lo[1]; u[2] &= hi[0]; u[3] &= hi[1];
+        a = __builtin_bit_cast(half8, u);
+      }
+      return a;
+    };
+    auto read_b = [&](int kk, int j) -> half8 {
+      const int row = wc * WN + j * 16 + fr;
+      half8 b = *reinterpret_cast<const half8*>(sbm + row * RB + (((kk * 4 + fg) ^ swzk(row)) << 4));
+      if constexpr (WKEEP) {  // zero this W row's Wanda-masked weights (8 k = chunk kk*4+fg); mask bit SET = removed
+        const unsigned mbyte = ~*reinterpret_cast<const unsigned char*>(sa + WKEEP_OFF + row * 8 + kk * 4 + fg);
+        const uint2v lo = *reinterpret_cast<const uint2v*>(smem + LUT_OFF + (mbyte & 15u) * 8);
+        const uint2v hi = *reinterpret_cast<const uint2v*>(smem + LUT_OFF + ((mbyte >> 4) & 15u) * 8);
+        uint4v u = __builtin_bit_cast(uint4v, b);
+        u[0] &= lo[0]; u[1] &= lo[1]; u[2] &= hi[0]; u[3] &= hi[1];
+        b = __builtin_bit_cast(half8, u);
+      }
+      return b;
+    };
+    if constexpr (SDMOE_GEMM_PIPE && !(KEEP && FN > 5)) {  // (wide masked tiles: no registers to spare)
+      // software-pipelined: A fragments in pairs, the next pair's LDS reads issued before the current pair's
+      // 2*FN MFMAs (one group of latency cover); the next kk's B fragments read during the last group when they
+      // fit a second register set. sched_barrier pins the read / MFMA order so hipcc cannot sink the reads to
+      // their first use (which exposes the LDS latency every group).
+      constexpr int NKK = BK / 32, NG = FM / 2;
+      constexpr bool BDB = FN <= 5 && !KEEP;  // second B set: +4*FN VGPRs (the masked modes need those registers)
+      half8 bcur[FN], bnxt[FN];
 #pragma unroll
-    for (int kk = 0; kk < BK / 32; ++kk) {
-      half8 af[FM], bf[FN];
+      for (int j = 0; j < FN; ++j) bcur[j] = read_b(0, j);
+      half8 a0 = read_a(0, 0), a1 = read_a(0, 1);
 #pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int row = wr * WM + i * 16 + fr;
-        af[i] = *reinterpret_cast<const half8*>(sa + row * RB + (((kk * 4 + fg) ^ swzk(row)) << 4));
-        if constexpr (AKEEP) {  // zero the neurons of this row's dropped experts (8 neurons = chunk kk*4+fg)
-          const unsigned kbyte = *reinterpret_cast<const unsigned char*>(sa + KEEP_OFF + row * 8 + kk * 4 + fg);
-          const uint2v lo = *reinterpret_cast<const uint2v*>(smem + LUT_OFF + (kbyte & 15u) * 8);
-          const uint2v hi = *reinterpret_cast<const uint2v*>(smem + LUT_OFF + (kbyte >> 4) * 8);
-          uint4v u = __builtin_bit_cast(uint4v, af[i]);
-          u[0] &= lo[0]; u[1] &= lo[1]; u[2] &= hi[0]; u[3] &= hi[1];
-          af[i] = __builtin_bit_cast(half8, u);
+      for (int kk = 0; kk < NKK; ++kk) {
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+          half8 n0 = a0, n1 = a1;
+          if (g + 1 < NG) {
+            n0 = read_a(kk, 2 * g + 2);
+            n1 = read_a(kk, 2 * g + 3);
+          } else if (kk + 1 < NKK) {
+            if constexpr (BDB) {
+#pragma unroll
+              for (int j = 0; j < FN; ++j) bnxt[j] = read_b(kk + 1, j);
+            }
+            n0 = read_a(kk + 1, 0);
+            n1 = read_a(kk + 1, 1);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[2 * g][j] = mfma16x16x32(a0, bcur[j], acc[2 * g][j]);
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[2 * g + 1][j] = mfma16x16x32(a1, bcur[j], acc[2 * g + 1][j]);
+          __builtin_amdgcn_sched_barrier(0);
+          a0 = n0;
+          a1 = n1;
+        }
+        if (kk + 1 < NKK) {
+#pragma unroll
+          for (int j = 0; j < FN; ++j) bcur[j] = BDB ? bnxt[j] : read_b(kk + 1, j);
         }
       }
+    } else {
 #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int row = wc * WN + j * 16 + fr;
-        bf[j] = *reinterpret_cast<const half8*>(sbm + row * RB + (((kk * 4 + fg) ^ swzk(row)) << 4));
-        if constexpr (WKEEP) {  // zero this W row's Wanda-masked weights (8 k = chunk kk*4+fg); mask bit SET = removed
-          const unsigned mbyte = ~*reinterpret_cast<const unsigned char*>(sa + WKEEP_OFF + row * 8 + kk * 4 + fg);
-          const uint2v lo = *reinterpret_cast<const uint2v*>(smem + LUT_OFF + (mbyte & 15u) * 8);
-          const uint2v hi = *reinterpret_cast<const uint2v*>(smem + LUT_OFF + ((mbyte >> 4) & 15u) * 8);
-          uint4v u = __builtin_bit_cast(uint4v, bf[j]);
-          u[0] &= lo[0]; u[1] &= lo[1]; u[2] &= hi[0]; u[3] &= hi[1];
-          bf[j] = __builtin_bit_cast(half8, u);
-        }
+      for (int kk = 0; kk < BK / 32; ++kk) {
+        half8 af[FM], bf[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) af[i] = read_a(kk, i);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bf[j] = read_b(kk, j);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32(af[i], bf[j], acc[i][j]);
       }
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32(af[i], bf[j], acc[i][j]);
     }
     if (p.prio) __builtin_amdgcn_s_setprio(0);
   }
@@ -426,6 +487,13 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
   // ---- epilogue: per wave, stage half of its fp32 tile (FM/2 fragment rows) in LDS at a time, then write
   // 8-column chunks with 16-B (fp16) / 32-B (fp32 split-K slab) stores
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (p.diag & 4) {  // diagnostics: keep the accumulators live, store nothing
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
   __syncthreads();
   float* st = reinterpret_cast<float*>(smem) + wave * (WM / NPASS) * WN_PAD;
   // GEGLU: this wave's WN bias values (fp32) copied once into LDS past the staging area (per wave, no block sync)
@@ -503,6 +571,7 @@ int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
   p.kchunk = (nk + p.ksplit - 1) / p.ksplit;
   p.part = p.ksplit > 1 ? ws : nullptr;
   p.prio = g_prio;
+  p.diag = g_diag;
   const dim3 grid(ntiles * p.ksplit);
   {
     // 64-deep K-steps (a 32-deep 4/5-stage ring measured slower on every shape; the kernel is generic in BK).
@@ -788,5 +857,6 @@ extern "C" int sdmoe_tune(int knob, int value) {
   if (knob == 1 && value >= 0 && value <= 5) { g_tile = value; return SDMOE_OK; }
   if (knob == 2 && (value == 0 || value == 32 || value == 64)) { g_bk = value; return SDMOE_OK; }
   if (knob == 3 && (value == 0 || value == 1)) { g_prio = value; return SDMOE_OK; }
+  if (knob == 6 && value >= 0 && value <= 7) { g_diag = value; return SDMOE_OK; }
   return SDMOE_EARG;
 }

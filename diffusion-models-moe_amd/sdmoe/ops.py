@@ -177,9 +177,24 @@ def linear(x, w, bias=None, *, out=None, residual=None, act=ACT_NONE, coladd=Non
     return out
 
 
+def conv_weight(w):
+    """Conv weight in the kernel's layout [Cout, Cin/64, 3, 3, 64] from [Cout, 3, 3, Cin] (taps-last NHWC filter)
+    or a torch [Cout, Cin, 3, 3] filter (pass nchw=True-shaped tensors through conv_weight_from_torch). K runs over
+    (64-channel slice, tap, channel): the 9 taps of one slice are consecutive K-steps of the implicit GEMM."""
+    Cout, kh, kw, Cin = w.shape
+    if (kh, kw) != (3, 3) or Cin % 64:
+        raise ValueError(f"conv_weight: expected [Cout, 3, 3, Cin] with Cin % 64 == 0, got {tuple(w.shape)}")
+    return w.reshape(Cout, 9, Cin // 64, 64).permute(0, 2, 1, 3).reshape(Cout, Cin // 64, 3, 3, 64).contiguous()
+
+
+def conv_weight_from_torch(w):
+    """torch.nn.Conv2d weight [Cout, Cin, 3, 3] -> conv_weight layout."""
+    return conv_weight(w.permute(0, 2, 3, 1))
+
+
 def conv3x3(x, nimg, H, W, w, bias=None, *, stride=1, upsample=False, out=None, residual=None, act=ACT_NONE,
             coladd=None, coladd_bstride=0, gn=None):
-    """3x3 conv (pad 1) on NHWC x viewed as [nimg*H*W, Cin]; w: [Cout, 3, 3, Cin] fp16.
+    """3x3 conv (pad 1) on NHWC x viewed as [nimg*H*W, Cin]; w: [Cout, Cin/64, 3, 3, 64] fp16 (conv_weight).
     gn = (scale, shift, silu): GroupNorm(+SiLU) applied to x once (one read + write of x) before the conv."""
     lib = _lib.load()
     if gn is not None:
@@ -187,8 +202,9 @@ def conv3x3(x, nimg, H, W, w, bias=None, *, stride=1, upsample=False, out=None, 
     xp, ldx = _rows(x, "x")
     Cin = x.shape[1]
     Cout = w.shape[0]
-    if tuple(w.shape[1:]) != (3, 3, Cin):
-        raise ValueError(f"conv3x3: weight {tuple(w.shape)} does not match Cin={Cin}")
+    if w.dim() != 5 or tuple(w.shape[1:]) != (Cin // 64, 3, 3, 64) or Cin % 64:
+        raise ValueError(f"conv3x3: weight {tuple(w.shape)} is not the [Cout, Cin/64, 3, 3, 64] layout for "
+                         f"Cin={Cin} (ops.conv_weight)")
     if x.shape[0] != nimg * H * W:
         raise ValueError("conv3x3: rows != nimg*H*W")
     if upsample:

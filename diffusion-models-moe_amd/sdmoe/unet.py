@@ -63,7 +63,7 @@ class LoRACompatibleLinear(nn.Module):
 
 
 class Conv2d(nn.Module):
-    """3x3 conv; weight stored [Cout, 3, 3, Cin] fp16 (K-contiguous implicit-GEMM layout)."""
+    """3x3 conv; weight stored [Cout, Cin/64, 3, 3, 64] fp16 (the implicit GEMM's K order, ops.conv_weight)."""
 
     def __init__(self, weight, bias, stride=1):
         super().__init__()
@@ -437,7 +437,7 @@ class UNet2DConditionModel(nn.Module):
             return LoRACompatibleLinear(t(p + ".weight"), t(p + ".bias") if bias else None)
 
         def conv(p, stride=1):
-            w = sd[p + ".weight"].to(dev, torch.float16).permute(0, 2, 3, 1).contiguous()
+            w = ops.conv_weight_from_torch(sd[p + ".weight"].to(dev, torch.float16))
             return Conv2d(w, t(p + ".bias"), stride)
 
         def conv1x1(p):
@@ -473,7 +473,7 @@ class UNet2DConditionModel(nn.Module):
                                       conv1x1(p + ".proj_out"))
 
         w_in = sd["conv_in.weight"].to(dev, torch.float16)
-        w_in = F.pad(w_in, (0, 0, 0, 0, 0, IN_PAD - w_in.shape[1])).permute(0, 2, 3, 1).contiguous()
+        w_in = ops.conv_weight_from_torch(F.pad(w_in, (0, 0, 0, 0, 0, IN_PAD - w_in.shape[1])))
         m.conv_in = Conv2d(w_in, t("conv_in.bias"))
         m.time_embedding = TimestepEmbedding(lin("time_embedding.linear_1"), lin("time_embedding.linear_2"))
         if cfg.addition_embed_type == "text_time":
@@ -505,7 +505,7 @@ class UNet2DConditionModel(nn.Module):
         m.up_blocks = nn.ModuleList(ups)
         m.conv_norm_out = gn("conv_norm_out", cfg.norm_eps)
         w_out = sd["conv_out.weight"].to(dev, torch.float16)
-        w_out = F.pad(w_out, (0, 0, 0, 0, 0, 0, 0, OUT_PAD - w_out.shape[0])).permute(0, 2, 3, 1).contiguous()
+        w_out = ops.conv_weight_from_torch(F.pad(w_out, (0, 0, 0, 0, 0, 0, 0, OUT_PAD - w_out.shape[0])))
         b_out = F.pad(sd["conv_out.bias"].to(dev, torch.float16), (0, OUT_PAD - cfg.out_channels)).contiguous()
         m.conv_out = Conv2d(w_out, b_out)
 

@@ -108,7 +108,7 @@ class AutoencoderKLDecoder:
             if cout_pad:
                 w = F.pad(w, (0, 0, 0, 0, 0, 0, 0, cout_pad - w.shape[0]))
                 b = F.pad(b, (0, cout_pad - b.shape[0]))
-            return w.half().permute(0, 2, 3, 1).contiguous(), b.half().contiguous()
+            return ops.conv_weight_from_torch(w.half()), b.half().contiguous()
 
         def resnet(p):
             r = {"n1": (h(p + ".norm1.weight"), h(p + ".norm1.bias")), "c1": conv(p + ".conv1"),

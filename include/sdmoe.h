@@ -47,7 +47,8 @@ int sdmoe_linear(const void* A, long lda, const void* W, long ldw, const void* b
 
 /*
  * 3x3 convolution, padding 1, on NHWC X [nimg, H, W, Cin] (pixel stride ldx): stride 1 or 2, or a fused
- * nearest-neighbour 2x upsample in front (upsample=1, output 2H x 2W). Weights [Cout][3][3][Cin].
+ * nearest-neighbour 2x upsample in front (upsample=1, output 2H x 2W). Weights [Cout][Cin/64][3][3][64]
+ * (torch [Cout, Cin, 3, 3] -> permute(0, 2, 3, 1) -> [Cout, 9, Cin/64, 64] -> [Cout, Cin/64, 9, 64]).
  * Same fused epilogue as sdmoe_linear (bias, per-image coladd = time embedding, activation, residual R).
  * Replaces: diffusers ResnetBlock2D conv1/conv2 (+temb add/residual), Downsample2D, Upsample2D,
  * conv_in/conv_out of UNet2DConditionModel (external). Requires Cin % 64 == 0, Cout % 8 == 0.

@@ -103,7 +103,7 @@ def test_conv3x3(Cin, Cout, H, stride, up):
     x = rnd(nimg * H * H, Cin, seed=20)
     w = rnd(Cout, 3, 3, Cin, scale=(9 * Cin) ** -0.5, seed=21)
     b = rnd(Cout, scale=0.1, seed=22)
-    out = ops.conv3x3(x, nimg, H, H, w, b, stride=stride, upsample=up)
+    out = ops.conv3x3(x, nimg, H, H, ops.conv_weight(w), b, stride=stride, upsample=up)
     close(out, conv_ref(x, nimg, H, H, w, b, stride, up))
 
 
@@ -115,7 +115,7 @@ def test_conv3x3_gn_silu_temb_residual():
     w, b = rnd(Cout, 3, 3, Cin, scale=(9 * Cin) ** -0.5, seed=26), rnd(Cout, scale=0.1, seed=27)
     temb = rnd(1, Cout, seed=28)
     res = rnd(nimg * H * H, Cout, seed=29)
-    out = ops.conv3x3(x, nimg, H, H, w, b, gn=(sc, sh, True), coladd=temb, coladd_bstride=0, residual=res)
+    out = ops.conv3x3(x, nimg, H, H, ops.conv_weight(w), b, gn=(sc, sh, True), coladd=temb, coladd_bstride=0, residual=res)
     xn = F.group_norm(x.float().view(nimg, H * H, Cin).permute(0, 2, 1), 32, gamma.float(), beta.float(), 1e-5)
     xn = F.silu(xn).permute(0, 2, 1).reshape(-1, Cin)
     ref = conv_ref(xn, nimg, H, H, w, b) + temb.float() + res.float()
@@ -126,9 +126,9 @@ def test_conv3x3_strided_concat_input():
     nimg, H, C1, C2, Cout = 2, 8, 640, 320, 320
     buf = rnd(nimg * H * H, C1 + C2, seed=30)
     w, b = rnd(Cout, 3, 3, C1 + C2, scale=(9 * (C1 + C2)) ** -0.5, seed=31), rnd(Cout, scale=0.1, seed=32)
-    close(ops.conv3x3(buf, nimg, H, H, w, b), conv_ref(buf, nimg, H, H, w, b))
+    close(ops.conv3x3(buf, nimg, H, H, ops.conv_weight(w), b), conv_ref(buf, nimg, H, H, w, b))
     w2 = rnd(Cout, 3, 3, C2, scale=(9 * C2) ** -0.5, seed=33)
-    close(ops.conv3x3(buf[:, C1:], nimg, H, H, w2, b), conv_ref(buf[:, C1:].contiguous(), nimg, H, H, w2, b))
+    close(ops.conv3x3(buf[:, C1:], nimg, H, H, ops.conv_weight(w2), b), conv_ref(buf[:, C1:].contiguous(), nimg, H, H, w2, b))
 
 
 @pytest.mark.parametrize("tile", [1, 2, 3, 4])
@@ -146,7 +146,7 @@ def test_forced_tiles(tile):
             xi = rnd(2 * H * H, Cin, seed=43)
             wi = rnd(Cout, 3, 3, Cin, scale=(9 * Cin) ** -0.5, seed=44)
             bi = rnd(Cout, scale=0.1, seed=45)
-            close(ops.conv3x3(xi, 2, H, H, wi, bi, stride=st, upsample=up), conv_ref(xi, 2, H, H, wi, bi, st, up))
+            close(ops.conv3x3(xi, 2, H, H, ops.conv_weight(wi), bi, stride=st, upsample=up), conv_ref(xi, 2, H, H, wi, bi, st, up))
     finally:
         _lib.check(lib.sdmoe_tune(1, 0), "tune")
 
@@ -323,7 +323,7 @@ def test_conv3x3_full_size_tiles(tile, stages):
     temb, res = rnd(1, C, seed=67), rnd(nimg * H * H, C, seed=68)
 
     def run():
-        out = ops.conv3x3(x, nimg, H, H, w, b, coladd=temb, coladd_bstride=0, residual=res)
+        out = ops.conv3x3(x, nimg, H, H, ops.conv_weight(w), b, coladd=temb, coladd_bstride=0, residual=res)
         close(out, conv_ref(x, nimg, H, H, w, b) + temb.float() + res.float())
     _with_tune([(1, tile), (0, stages)], run)
 
@@ -333,10 +333,10 @@ def test_conv3x3_full_size_upsample_concat():
     nimg = 16
     x = rnd(nimg * 32 * 32, 640, seed=69)
     w, b = rnd(640, 3, 3, 640, scale=(9 * 640) ** -0.5, seed=70), rnd(640, scale=0.1, seed=71)
-    close(ops.conv3x3(x, nimg, 32, 32, w, b, upsample=True), conv_ref(x, nimg, 32, 32, w, b, 1, True))
+    close(ops.conv3x3(x, nimg, 32, 32, ops.conv_weight(w), b, upsample=True), conv_ref(x, nimg, 32, 32, w, b, 1, True))
     buf = rnd(nimg * 64 * 64, 960, seed=72)
     w2 = rnd(320, 3, 3, 960, scale=(9 * 960) ** -0.5, seed=73)
-    close(ops.conv3x3(buf, nimg, 64, 64, w2, b[:320]), conv_ref(buf, nimg, 64, 64, w2, b[:320]))
+    close(ops.conv3x3(buf, nimg, 64, 64, ops.conv_weight(w2), b[:320]), conv_ref(buf, nimg, 64, 64, w2, b[:320]))
 
 
 @pytest.mark.parametrize("C,HW", [(320, 4096), (640, 4096), (960, 4096)])

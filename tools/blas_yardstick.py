@@ -35,7 +35,7 @@ for M, N, K, conv in [(n * 4096, 320, 2880, (64, 320)), (n * 1024, 640, 5760, (3
     if conv:
         H, C = conv
         x = torch.randn(n * H * H, C, device="cuda").half()
-        w = (torch.randn(C, 3, 3, C, device="cuda") * (9 * C) ** -0.5).half()
+        w = ops.conv_weight((torch.randn(C, 3, 3, C, device="cuda") * (9 * C) ** -0.5).half())
         ms2 = t(lambda: ops.conv3x3(x, n, H, H, w))
         line += f" | sdmoe conv3x3 {2 * M * N * K / ms2 / 1e9:7.1f} TF/s"
     else:

@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--bk", type=int, default=0, help="GEMM K-step depth (sdmoe_tune knob 2), 0 = auto")
     ap.add_argument("--prio", type=int, default=0, help="s_setprio around the MFMA block (knob 3)")
     ap.add_argument("--nqf", type=int, default=0, help="attention query fragments per wave (knob 4), 0 = auto")
+    ap.add_argument("--diag", type=int, default=0, help="GEMM diagnostics (knob 6, bits): 1 = no K-loop loads, 2 = no MFMA, 4 = no epilogue")
     a = ap.parse_args()
     from sdmoe import _lib
     _lib.check(_lib.load().sdmoe_tune(0, a.stages), "tune")
@@ -42,6 +43,7 @@ def main():
     _lib.check(_lib.load().sdmoe_tune(2, a.bk), "tune")
     _lib.check(_lib.load().sdmoe_tune(3, a.prio), "tune")
     _lib.check(_lib.load().sdmoe_tune(4, a.nqf), "tune")
+    _lib.check(_lib.load().sdmoe_tune(6, a.diag), "tune")
     print("stages", a.stages, "tile", a.tile, "bk", a.bk)
     n = a.nimg
     dev = "cuda"
@@ -52,7 +54,7 @@ def main():
                                   (8, 1280, 1280, 1, 0), (8, 2560, 1280, 1, 0), (64, 320, 320, 2, 0),
                                   (32, 640, 640, 1, 1), (64, 320, 8, 1, 0)]:
         x = torch.randn(n * H * H, Cin, device=dev).half()
-        w = (torch.randn(Cout, 3, 3, Cin, device=dev) * (9 * Cin) ** -0.5).half()
+        w = ops.conv_weight((torch.randn(Cout, 3, 3, Cin, device=dev) * (9 * Cin) ** -0.5).half())
         b = torch.zeros(Cout, device=dev).half()
         OH = 2 * H if up else (H - 1) // st + 1
         ms = timeit(lambda: ops.conv3x3(x, n, H, H, w, b, stride=st, upsample=bool(up)), a.iters)

@@ -25,7 +25,7 @@ def main():
         f = lambda: ops.attention(q[:, :C], q[:, C:2 * C], q[:, 2 * C:], n, 4096, 4096, 8)  # noqa: E731
     elif a.what == "conv":
         x = torch.randn(n * 4096, 320, device=dev).half()
-        w = (torch.randn(320, 3, 3, 320, device=dev) * 0.02).half()
+        w = ops.conv_weight((torch.randn(320, 3, 3, 320, device=dev) * 0.02).half())
         f = lambda: ops.conv3x3(x, n, 64, 64, w)  # noqa: E731
     else:
         x = torch.randn(n * 4096, 320, device=dev).half()

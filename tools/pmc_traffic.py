@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--mode", default="1,2", help="comma list of gemm_kernel MODE values (5th template arg: "
                     "1 = conv, 2 = conv with fused upsample); '' = any")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--build", default="", help="git revision of the measured build (recorded in the json)")
     a = ap.parse_args()
     fetch, names = load(a.fetch_csv, "FETCH_SIZE")
     write, wnames = load(a.write_csv, "WRITE_SIZE")
@@ -56,7 +57,8 @@ def main():
     res = {"kernel": a.kernel, "mode": a.mode, "launches_fetch": len(f_sel), "launches_write": len(w_sel),
            "fetch_bytes_per_launch": fetch_b, "write_bytes_per_launch": write_b,
            "bytes_per_launch": fetch_b + write_b,
-           "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), WRITE_SIZE x1; KiB -> bytes"}
+           "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), WRITE_SIZE x1; KiB -> bytes",
+           "build": a.build}
     print(json.dumps(res, indent=1))
     if a.out:
         json.dump(res, open(a.out, "w"), indent=1)
