@@ -309,7 +309,265 @@ __global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn_fwd_kernel(AttnP
   }
 }
 
-int g_attn_nqf = 0;  // sdmoe_tune knob 4: query fragments per wave (0 = auto, 2 or 4)
+// ---------------------------------------------------------------------------------------------------------------
+// attn32_kernel: the same flash-style forward on v_mfma_f32_32x32x16_f16, both products with the QUERY ON THE LANE:
+//   S^T (32 keys x 32 queries per MFMA block) = K Q^T   -- A = K rows from LDS (ds_read_b128), B = Q^T in registers;
+//   O^T (32 d x 32 queries)                   = V^T P^T -- A = V^T by ds_read_b64_tr_b16, B = P^T straight from the
+//     S^T accumulator registers (registers 8s..8s+7 of a block = k-step s; the V^T reads use the same permuted keys).
+// So the online-softmax state (running max m, sum l, the rescale of O) stays lane-local. Against the 16x16x32 kernel:
+// half the MFMA instructions per tile (14 vs 28 at d = 40: each issue slot an MFMA holds is VALU time lost), the QK
+// contraction padded only to 16 (40 -> 48, not 64), the exp2 argument -m kept as a persistent C operand (reloaded
+// only when the deferred rescale moves m), one cross-lane max per tile.
+// Row sums: by MFMA through a ones column at d = D where D % 32 leaves room in the last O^T block (d = 40, 80; the
+// lanes that would read V column D read a constant [1 0 0 0] block instead), else as VALU partial sums.
+// 4 waves x 32 queries per workgroup, 64-key K/V tiles in a double-buffered LDS-DMA ring, one barrier per tile.
+typedef float float16v __attribute__((ext_vector_type(16)));
+
+SDMOE_DEV float16v mfma32x32x16(half8 a, half8 b, float16v c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+template <int D>
+__global__ __launch_bounds__(256, (D <= 40 ? 4 : (D >= 160 ? 1 : 2))) void attn32_kernel(AttnParams p) {
+  constexpr int NQC = (D + 15) / 16;                  // 16-deep QK contraction steps (d zero-padded to 16 NQC)
+  constexpr int DQ = 16 * NQC;
+  constexpr bool SUM_MFMA = (D % 32) != 0 && (D % 4) == 0;  // ones column at d = D inside the last O^T block
+  // -m through the QK contraction when it has a spare column (d = 40 -> 48): K[:, D] := 1 (one ds_write per lane per
+  // tile into the row's pad slot) and Q~[:, D] := -m (fp16), so S' = K Q~^T - m needs no C operand at all; else the
+  // score MFMAs start from a 16-register -m vector
+  constexpr bool ONES_K = (D % 16) == 8;
+  constexpr int NDB = (D + (SUM_MFMA ? 1 : 0) + 31) / 32;   // 32-row blocks of O^T
+  constexpr int KB = 64;                              // keys per tile
+  constexpr int RS = DQ + 8;                          // K/V row stride (halves): RS/8 odd -> conflict-free K reads
+  static_assert((RS / 8) % 2 == 1, "row stride must be an odd number of 16-B slots");
+  constexpr int CH = D / 8;                           // real 16-B chunks per row (the rest load as zeros)
+  constexpr int SL = RS / 8;
+  constexpr int TILE = KB * RS;
+  constexpr int NPIECE = TILE * 2 / 1024;             // 1-KiB LDS-DMA wave-instructions per K (or V) tile
+  static_assert(NPIECE * 1024 == TILE * 2, "tile must be whole 1-KiB pieces");
+  constexpr int NPW = (2 * NPIECE + 3) / 4;           // per wave (the last round partly empty)
+  constexpr int TAIL = 64;                            // O^T blocks past RS over-read the last V row (discarded rows)
+  constexpr int VOFF = TILE + TAIL, COFF = VOFF + TILE + TAIL, SLOT = COFF + 8;
+  constexpr float RESCALE_THR = 8.0f;
+  constexpr unsigned OOB = 0x80000000u;
+  __shared__ __attribute__((aligned(1024))) half_t S0[SLOT];
+  __shared__ __attribute__((aligned(1024))) half_t S1[SLOT];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ln = lane & 31, hf = lane >> 5;           // query column of the MFMA blocks, lane half
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int q0 = blockIdx.x * 128 + wave * 32;
+
+  const half_t* Qb = p.Q + (long)b * p.Nq * p.ldq + h * D;
+  const half_t* Kb = p.K + (long)b * p.Nk * p.ldk + h * D;
+  const half_t* Vb = p.V + (long)b * p.Nk * p.ldv + h * D;
+  const __amdgpu_buffer_rsrc_t rsK =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Kb, (short)0, (int)(((long)p.Nk - 1) * p.ldk * 2 + D * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsV =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Vb, (short)0, (int)(((long)p.Nk - 1) * p.ldv * 2 + D * 2), 0x00020000);
+
+  unsigned voff[NPW], vstep[NPW];
+  int ldsoff[NPW];
+#pragma unroll
+  for (int j = 0; j < NPW; ++j) {
+    const int gp = wave + 4 * j;
+    const bool isk = gp < NPIECE;
+    const int pc = isk ? gp : gp - NPIECE;
+    const int slot = pc * 64 + lane, r = slot / SL, c = slot - (slot / SL) * SL;
+    const long ld = isk ? p.ldk : p.ldv;
+    voff[j] = c < CH ? (unsigned)(r * ld * 2 + c * 16) : OOB;
+    vstep[j] = (unsigned)(KB * ld * 2);
+    ldsoff[j] = (isk ? 0 : VOFF) + pc * 512;
+  }
+  auto issue_tile = [&](half_t* Sd) {
+#pragma unroll
+    for (int j = 0; j < NPW; ++j) {
+      if (wave + 4 * j < 2 * NPIECE) bld16(wave + 4 * j < NPIECE ? rsK : rsV, Sd + ldsoff[j], voff[j]);
+      voff[j] += vstep[j];
+    }
+  };
+
+  for (int i = tid; i < TAIL; i += 256) S0[TILE + i] = S1[TILE + i] = S0[VOFF + TILE + i] = S1[VOFF + TILE + i] = 0;
+  if (tid < 8) S0[COFF + tid] = S1[COFF + tid] = (half_t)(tid == 0 ? 1.f : 0.f);
+
+  const int nkt = (p.Nk + KB - 1) / KB;
+  issue_tile(S0);
+
+  // Q^T fragments (B operand): lane holds Q[q0 + ln][16c + 8hf .. +8], prescaled by scale*log2(e) so the score
+  // accumulator is already exp2's argument; zero past D and past Nq
+  half8 qf[NQC];
+#pragma unroll
+  for (int c = 0; c < NQC; ++c) {
+    const int q = q0 + ln, d = 16 * c + 8 * hf;
+    half8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (q < p.Nq && d < D) v = *reinterpret_cast<const half8*>(Qb + (long)q * p.ldq + d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (half_t)((float)v[j] * p.scale_log2);
+    qf[c] = v;
+  }
+
+  float16v oacc[NDB];
+#pragma unroll
+  for (int db = 0; db < NDB; ++db) oacc[db] = (float16v)(0.f);
+  float16v negm = (float16v)(0.f);  // -m in every register: the initial accumulator of the score MFMAs (!ONES_K)
+  float mrun = 0.f, lrun = 0.f;      // ONES_K: mrun is the fp16-representable shift actually in Q~[:, D]
+  auto set_shift = [&](float m) {    // lanes of the upper half hold d = 16 (NQC-1) + 8 = D in element 0
+    if constexpr (ONES_K) {
+      if (hf) qf[NQC - 1][0] = (half_t)(-m);
+    } else {
+      negm = (float16v)(-m);
+    }
+  };
+
+  // V^T operand addresses: lane (group g16 = lane / 16, index 4 tq + tp in it) supplies row 4 hf + tq (+ 8 for the
+  // second read) and columns 16 (g16 & 1) + 4 tp of its 4 x 16 transposed-read block
+  const int gi = lane & 15, g16 = lane >> 4, tq = gi >> 2, tp = gi & 3;
+  const int vbase = VOFF + (4 * hf + tq) * RS + 16 * (g16 & 1) + 4 * tp;
+  const bool onecol = SUM_MFMA && (g16 & 1) == (D % 32) / 16 && tp == (D % 16) / 4;
+
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  auto tile = [&](int kt, auto ragged_tag, auto buf_tag, auto first_tag) {
+    constexpr bool RAGGED = decltype(ragged_tag)::value;
+    constexpr int BUF = decltype(buf_tag)::value;
+    constexpr bool FIRST = decltype(first_tag)::value;  // the first tile sets m (peeled: no runtime merge of states)
+    const half_t* St = BUF ? S1 : S0;
+    if (kt + 1 < nkt) issue_tile(BUF ? S0 : S1);
+    if constexpr (ONES_K) const_cast<half_t*>(St)[lane * RS + D] = (half_t)1.f;  // K[key][D] = 1 for this tile
+
+    // ---- S^T = K Q~^T - m (two 32-key blocks)
+    float16v s[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      s[kb] = (FIRST || ONES_K) ? (float16v)(0.f) : negm;
+#pragma unroll
+      for (int c = 0; c < NQC; ++c) {
+        const half8 a = *reinterpret_cast<const half8*>(St + (32 * kb + ln) * RS + 16 * c + 8 * hf);
+        s[kb] = mfma32x32x16(a, qf[c], s[kb]);
+      }
+    }
+    if constexpr (RAGGED) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (kt * KB + 32 * kb + (r & 3) + 8 * (r >> 2) + 4 * hf >= p.Nk) s[kb][r] = -INFINITY;
+    }
+    // ---- online softmax, query on the lane: 32 scores here, the other 32 keys in lane ^ 32
+    float m4[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) m4[i] = max3(s[i >> 2][(i & 3) * 4], s[i >> 2][(i & 3) * 4 + 1], s[i >> 2][(i & 3) * 4 + 2]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) m4[i] = max2(m4[i], s[i >> 2][(i & 3) * 4 + 3]);
+    float mx = max3(max3(m4[0], m4[1], m4[2]), max3(m4[3], m4[4], m4[5]), max2(m4[6], m4[7]));
+    {
+      auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+      mx = max2(__uint_as_float(r[0]), __uint_as_float(r[1]));
+    }
+    if constexpr (FIRST) {  // first tile: m = its max (O and l are still zero)
+      mrun = ONES_K ? (float)(half_t)mx : mx;
+      set_shift(mrun);
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) s[kb] -= mrun;
+    } else if (!__all(mx <= RESCALE_THR)) {  // wave-uniform: deferred rescale (p <= 2^8 keeps fp16 safe)
+      const float mnew = ONES_K ? (float)(half_t)(mrun + fmaxf(mx, 0.f)) : mrun + fmaxf(mx, 0.f);
+      const float delta = mnew - mrun;  // exact: the shifts old and new are both in use as given
+      mrun = mnew;
+      set_shift(mrun);
+      const float alpha = __builtin_amdgcn_exp2f(-delta);
+      if (!SUM_MFMA) lrun *= alpha;
+#pragma unroll
+      for (int db = 0; db < NDB; ++db) oacc[db] *= alpha;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) s[kb] -= delta;
+    }
+    // ---- P = exp2(S'), packed to fp16 k-step fragments: registers 8cs..8cs+7 of block kb = keys 16cs + ...
+    half8 pb[2][2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      float ls = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float e = __builtin_amdgcn_exp2f(s[kb][r]);
+        if (!SUM_MFMA) ls += e;
+        pb[kb][r >> 3][r & 7] = (half_t)e;
+      }
+      if (!SUM_MFMA) lrun += ls;
+    }
+    // ---- O^T += V^T P^T over the four 16-key steps
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int cs = 0; cs < 2; ++cs)
+#pragma unroll
+        for (int db = 0; db < NDB; ++db) {
+          const half_t* a1 = St + vbase + (32 * kb + 16 * cs) * RS + 32 * db;
+          const half_t* a2 = a1 + 8 * RS;
+          if (SUM_MFMA && db == NDB - 1 && onecol) a1 = a2 = St + COFF;
+          const half4 lo = ds_read_tr(a1), hi = ds_read_tr(a2);
+          const half8 a = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          oacc[db] = mfma32x32x16(a, pb[kb][cs], oacc[db]);
+        }
+
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of tile kt+1 have landed
+    __syncthreads();
+  };
+
+  using F_ = std::integral_constant<bool, false>;
+  using T_ = std::integral_constant<bool, true>;
+  using B0 = std::integral_constant<int, 0>;
+  using B1 = std::integral_constant<int, 1>;
+  const int nfull = p.Nk / KB;
+  int kt = 0;
+  if (nfull == 0) {  // a single ragged tile (Nk < 64)
+    tile(0, T_(), B0(), T_());
+    kt = 1;
+  } else {
+    tile(0, F_(), B0(), T_());
+    kt = 1;
+    for (; kt + 1 < nfull; kt += 2) {
+      tile(kt, F_(), B1(), F_());
+      tile(kt + 1, F_(), B0(), F_());
+    }
+    if (kt < nfull) { tile(kt, F_(), B1(), F_()); ++kt; }
+    if (kt < nkt) {
+      if (kt & 1) tile(kt, T_(), B1(), F_());
+      else tile(kt, T_(), B0(), F_());
+    }
+  }
+
+  // ---- normalise and store: lane (query q0 + ln) holds O^T rows d = 32 db + 8 t + 4 hf + 0..3 in registers 4t..4t+3
+  float l;
+  if constexpr (SUM_MFMA) {
+    constexpr int HD = ((D % 32) >> 2) & 1, TD = (D % 32) >> 3;
+    l = __shfl(oacc[D / 32][4 * TD], HD * 32 + ln, 64);
+  } else {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(lrun), __float_as_uint(lrun), false, false);
+    l = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  const float inv = 1.0f / l;
+  const int q = q0 + ln;
+  if (q >= p.Nq) return;
+  half_t* Orow = p.O + (long)b * p.Nq * p.ldo + h * D + (long)q * p.ldo;
+#pragma unroll
+  for (int db = 0; db < NDB; ++db)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int d = 32 * db + 8 * t + 4 * hf;
+      if (d < D) {
+        half4 o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = (half_t)(oacc[db][4 * t + i] * inv);
+        *reinterpret_cast<half4*>(Orow + d) = o;
+      }
+    }
+}
+
+// sdmoe_tune knob 4: 0 = by shape (default): attn32_kernel for d = 80 self-attention (Nk > 128), the 16x16x32
+// kernel (NQF = 2) everywhere else; 1 = attn32_kernel; 2 or 4 = the 16x16x32 kernel with NQF = 2 / 4
+int g_attn_nqf = 0;
 
 template <int D>
 int launch(const AttnParams& p, int nimg, hipStream_t s) {
@@ -318,7 +576,16 @@ int launch(const AttnParams& p, int nimg, hipStream_t s) {
   // head dims above 40 would spill at NQF = 4 (64: 16 VGPRs, 80: 130)
   constexpr bool WIDE_OK = D <= 40;
   const bool wide = g_attn_nqf == 4;
-  if (WIDE_OK && wide) {
+  // same-box timings, 16 images x 8 heads, 16x16x32 vs 32x32x16 (us): d = 40 N = 4096 self 499 vs 524, 77-key cross
+  // 34.1 vs 41.0; d = 64 N = 4096 630 vs 645, cross 43.4 vs 50.8; d = 80 N = 1024 self 66.9 vs 64.0 (the contraction
+  // 80 -> 80 instead of 96), cross 21.4 vs 22.2; d = 160 19.2 vs 19.5. The 32x32x16 loop issues fewer instructions
+  // (14 MFMAs and ~100 VALU per 64-key tile vs 28 and ~110 at d = 40) but runs slower: lower clock under DVFS for
+  // the 32x32 MFMA (MI355X_MICROARCH.md) and 2-way LDS bank conflicts on its V^T transpose reads (row stride 56)
+  const bool use32 = g_attn_nqf == 1 || (g_attn_nqf == 0 && D == 80 && p.Nk > 128);
+  if (use32) {
+    dim3 grid((p.Nq + 127) / 128, p.heads, nimg);
+    attn32_kernel<D><<<grid, 256, 0, s>>>(p);
+  } else if (WIDE_OK && wide) {
     dim3 grid((p.Nq + 255) / 256, p.heads, nimg);
     attn_fwd_kernel<D, (WIDE_OK ? 4 : 2)><<<grid, 256, 0, s>>>(p);
   } else {
@@ -332,7 +599,7 @@ int launch(const AttnParams& p, int nimg, hipStream_t s) {
 }  // namespace
 
 int sdmoe_attn_set_nqf(int v) {
-  if (v != 0 && v != 2 && v != 4) return SDMOE_EARG;
+  if (v != 0 && v != 1 && v != 2 && v != 4) return SDMOE_EARG;
   g_attn_nqf = v;
   return SDMOE_OK;
 }

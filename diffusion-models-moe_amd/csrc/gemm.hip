@@ -35,7 +35,7 @@ int g_tile = 0;
 int g_bk = 0;
 int g_prio = 0;
 int g_diag = 0;  // knob 6, diagnostics only (results garbage): bit 0 = no K-loop operand loads, bit 1 = no MFMAs,
-                 // bit 2 = no epilogue (nothing stored)
+                 // bit 2 = no epilogue (nothing stored), bit 3 = epilogue without its global stores
 int g_sched = 0;  // knob 6, diagnostics only: bit 0 = no K-loop operand loads, bit 1 = no MFMAs (results garbage)
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -105,6 +105,10 @@ SDMOE_DEV void epilogue8(const GemmParams& p, int m, int n, float (&v)[8]) {
   half8 o;
 #pragma unroll
   for (int j = 0; j < 8; ++j) o[j] = (half_t)v[j];
+  if (p.diag & 8) {  // diagnostics: everything but the global store
+    asm volatile("" ::"v"(o));
+    return;
+  }
   *reinterpret_cast<half8*>(p.C + (long)m * p.ldc + n) = o;
 }
 
@@ -857,6 +861,6 @@ extern "C" int sdmoe_tune(int knob, int value) {
   if (knob == 1 && value >= 0 && value <= 5) { g_tile = value; return SDMOE_OK; }
   if (knob == 2 && (value == 0 || value == 32 || value == 64)) { g_bk = value; return SDMOE_OK; }
   if (knob == 3 && (value == 0 || value == 1)) { g_prio = value; return SDMOE_OK; }
-  if (knob == 6 && value >= 0 && value <= 7) { g_diag = value; return SDMOE_OK; }
+  if (knob == 6 && value >= 0 && value <= 15) { g_diag = value; return SDMOE_OK; }
   return SDMOE_EARG;
 }

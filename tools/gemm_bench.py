@@ -34,7 +34,7 @@ def main():
     ap.add_argument("--only", default="", help="run only rows whose label contains this")
     ap.add_argument("--bk", type=int, default=0, help="GEMM K-step depth (sdmoe_tune knob 2), 0 = auto")
     ap.add_argument("--prio", type=int, default=0, help="s_setprio around the MFMA block (knob 3)")
-    ap.add_argument("--nqf", type=int, default=0, help="attention query fragments per wave (knob 4), 0 = auto")
+    ap.add_argument("--nqf", type=int, default=0, help="attention kernel (knob 4): 0 = auto, 1 = 32x32x16, 2/4 = 16x16x32 NQF")
     ap.add_argument("--diag", type=int, default=0, help="GEMM diagnostics (knob 6, bits): 1 = no K-loop loads, 2 = no MFMA, 4 = no epilogue")
     a = ap.parse_args()
     from sdmoe import _lib
@@ -105,7 +105,8 @@ def main():
         rows.append((f"  unfused proj M={M} N={2 * F} K={C}", ms, 2.0 * M * 2 * F * C / ms / 1e9))
         ms = timeit(lambda: ops.geglu_route(y, routing, ops.ACT_RELU, out=out), a.iters)
         rows.append((f"  unfused route M={M} F={F} (GB/s)", ms, (M * F * 6) / ms / 1e6))
-    for N_, d, Nk in [(4096, 40, 4096), (4096, 40, 77), (1024, 80, 1024), (256, 160, 256)]:
+    for N_, d, Nk in [(4096, 40, 4096), (4096, 40, 77), (1024, 80, 1024), (1024, 80, 77), (256, 160, 256),
+                      (256, 160, 77), (4096, 64, 4096), (4096, 64, 77), (1024, 64, 1024)]:
         C = 8 * d
         q = torch.randn(n * N_, 3 * C, device=dev).half()
         kv = torch.randn(n * Nk, 2 * C, device=dev).half()
