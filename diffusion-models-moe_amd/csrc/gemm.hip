@@ -631,7 +631,12 @@ int dispatch(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
   // Measured on MI355X with tools/gemm_bench.py --tile.
   const int nt320 = tm256 * (p.N / 320);
   const int nt160_128 = ((p.M + 127) / 128) * ((p.N + 159) / 160);
-  if (p.N % 320 == 0 && nt320 >= 240) return launch_tile<256, 320, 2, 4, MODE>(p, ws, ws_floats, s);
+  // The keep-masked A operand (routed FFN down projection) takes the 4x2-wave arrangement (wave tile 64x160: half
+  // the A fragments to mask per wave): 61 vs 69 us at M = 65536, N = 320, K = 1280 (tools/gemm_bench.py --tile 5).
+  if (p.N % 320 == 0 && nt320 >= 240) {
+    if constexpr (mode_akeep(MODE)) return launch_tile<256, 320, 4, 2, MODE>(p, ws, ws_floats, s);
+    return launch_tile<256, 320, 2, 4, MODE>(p, ws, ws_floats, s);
+  }
   // 1-1.25 waves of 128x160 tiles (M = 4096 x N = 1280 projections at the 16x16 level): 64x160 tiles double
   // the grid to two workgroups per CU — 15-18 % faster in isolation (tools/gpu_tiles_all.sh). Convs keep their
   // tiles: with the convs included the same-box pipeline A/B measured 0.5 % slower.
