@@ -36,7 +36,6 @@ int g_bk = 0;
 int g_prio = 0;
 int g_diag = 0;  // knob 6, diagnostics only (results garbage): bit 0 = no K-loop operand loads, bit 1 = no MFMAs,
                  // bit 2 = no epilogue (nothing stored), bit 3 = epilogue without its global stores
-int g_sched = 0;  // knob 6, diagnostics only: bit 0 = no K-loop operand loads, bit 1 = no MFMAs (results garbage)
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
@@ -131,20 +130,34 @@ constexpr int KEEP_LUT_BYTES = 16 * 8;  // 4 keep bits -> 4 x 16-bit lane masks
 // Routed-GEGLU epilogue over one staged pass (rows x WN fp32 in LDS, row stride WN_PAD) of a wave's tile
 // whose columns n0..n0+WN-1 are [value 8 | gate 8] chunk pairs. Rounds exactly like the unfused path
 // (fp16 linear output, fp16 act, fp16 product; expert score = fp32 sum in neuron order, rounded to fp16).
-template <int S, int WN, int WN_PAD>
-SDMOE_DEV void expert_sums(const GemmParams& p, const float* st, int mrow0, int rows, int n0, int lane) {
+// LDS access is row-fastest (lane -> row id % ROWS): the 16 lanes of a b128 access phase then read 16 rows of one
+// column, which the odd 16-B row stride (WN_PAD = WN + 4) spreads over all 64 banks. (Column-fastest, 16 floats apart
+// per lane, was 3-way conflicted: 1.9e7 conflict cycles per launch at 64x64.)
+template <int S, int WN, int WN_PAD, int ROWS>
+SDMOE_DEV void expert_sums(const GemmParams& p, const float* st, int mrow0, int n0, int lane) {
   constexpr int NE = (WN / 2) / S;
-  for (int id = lane; id < rows * NE; id += 64) {
-    const int r = id / NE, e = id - r * NE;
+  for (int id = lane; id < ROWS * NE; id += 64) {
+    const int r = id % ROWS, e = id / ROWS;
     const int m = mrow0 + r;
     const float* rp = st + r * WN_PAD + 8;
     float v[S];
+    if constexpr (S % 4 == 0) {  // whole aligned quads of one gate chunk: b128 reads
 #pragma unroll
-    for (int t = 0; t < S; ++t) v[t] = rp[16 * ((e * S + t) >> 3) + ((e * S + t) & 7)];
+      for (int q = 0; q < S / 4; ++q) {
+        const int nn = e * S + 4 * q;
+        const float4v x = *reinterpret_cast<const float4v*>(rp + 16 * (nn >> 3) + (nn & 7));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[4 * q + i] = x[i];
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < S; ++t) v[t] = rp[16 * ((e * S + t) >> 3) + ((e * S + t) & 7)];
+    }
     float acc = 0.f;
 #pragma unroll
     for (int t = 0; t < S; ++t) acc += v[t];  // neuron order, as the unfused kernel
-    if (m < p.M) p.score[(long)m * p.ld_score + n0 / 2 / S + e] = (half_t)acc;
+    if (p.diag & 8) asm volatile("" ::"v"(acc));
+    else if (m < p.M) p.score[(long)m * p.ld_score + n0 / 2 / S + e] = (half_t)acc;
   }
 }
 
@@ -158,17 +171,24 @@ SDMOE_DEV void geglu_pass(const GemmParams& p, float* st, int mrow0, int n0, int
   for (int it = 0; it < (ROWS * PPR + 63) / 64; ++it) {
     const int id = lane + 64 * it;
     if (id >= rows * PPR) break;
-    const int r = id / PPR, j = id - r * PPR;
+    const int r = id % rows, j = id / rows;  // row-fastest: conflict-free b128 LDS phases (see expert_sums)
     const int m = mrow0 + r, n = n0 + 16 * j;
     float* sp = st + r * WN_PAD + 16 * j;
     const float* bp = gbias + 16 * j;
+    float x[16], bb[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4v a = *reinterpret_cast<const float4v*>(sp + 4 * q), c = *reinterpret_cast<const float4v*>(bp + 4 * q);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { x[4 * q + i] = a[i]; bb[4 * q + i] = c[i]; }
+    }
     // fp16 linear outputs (fp32 acc + bias, rounded once), then act / product on packed halves: the product of
     // two fp16 values is exact in fp32, so the packed fp16 multiply rounds identically
     h2 yh[4], yg[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      yh[t] = (h2){(half_t)(sp[2 * t] + bp[2 * t]), (half_t)(sp[2 * t + 1] + bp[2 * t + 1])};
-      yg[t] = (h2){(half_t)(sp[8 + 2 * t] + bp[8 + 2 * t]), (half_t)(sp[9 + 2 * t] + bp[9 + 2 * t])};
+      yh[t] = (h2){(half_t)(x[2 * t] + bb[2 * t]), (half_t)(x[2 * t + 1] + bb[2 * t + 1])};
+      yg[t] = (h2){(half_t)(x[8 + 2 * t] + bb[8 + 2 * t]), (half_t)(x[9 + 2 * t] + bb[9 + 2 * t])};
     }
     h2 ga[4];
     if (p.act == ACT_RELU) {
@@ -189,21 +209,22 @@ SDMOE_DEV void geglu_pass(const GemmParams& p, float* st, int mrow0, int n0, int
     // the activated gate, for the expert sums
     *reinterpret_cast<float4v*>(sp + 8) = (float4v){(float)ga[0][0], (float)ga[0][1], (float)ga[1][0], (float)ga[1][1]};
     *reinterpret_cast<float4v*>(sp + 12) = (float4v){(float)ga[2][0], (float)ga[2][1], (float)ga[3][0], (float)ga[3][1]};
-    if (m < p.M) *reinterpret_cast<half8*>(p.C + (long)m * p.ldc + n / 2) = o;
+    if (p.diag & 8) asm volatile("" ::"v"(o));  // diagnostics: no global store
+    else if (m < p.M) *reinterpret_cast<half8*>(p.C + (long)m * p.ldc + n / 2) = o;
   }
   if (!p.score) return;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   switch (p.esize) {
-    case 20: expert_sums<20, WN, WN_PAD>(p, st, mrow0, rows, n0, lane); break;
-    case 10: expert_sums<10, WN, WN_PAD>(p, st, mrow0, rows, n0, lane); break;
-    case 40: expert_sums<40, WN, WN_PAD>(p, st, mrow0, rows, n0, lane); break;
-    case 8: expert_sums<8, WN, WN_PAD>(p, st, mrow0, rows, n0, lane); break;
-    case 5: expert_sums<5, WN, WN_PAD>(p, st, mrow0, rows, n0, lane); break;
-    case 4: expert_sums<4, WN, WN_PAD>(p, st, mrow0, rows, n0, lane); break;
-    case 2: expert_sums<2, WN, WN_PAD>(p, st, mrow0, rows, n0, lane); break;
-    default: expert_sums<1, WN, WN_PAD>(p, st, mrow0, rows, n0, lane); break;
+    case 20: expert_sums<20, WN, WN_PAD, ROWS>(p, st, mrow0, n0, lane); break;
+    case 10: expert_sums<10, WN, WN_PAD, ROWS>(p, st, mrow0, n0, lane); break;
+    case 40: expert_sums<40, WN, WN_PAD, ROWS>(p, st, mrow0, n0, lane); break;
+    case 8: expert_sums<8, WN, WN_PAD, ROWS>(p, st, mrow0, n0, lane); break;
+    case 5: expert_sums<5, WN, WN_PAD, ROWS>(p, st, mrow0, n0, lane); break;
+    case 4: expert_sums<4, WN, WN_PAD, ROWS>(p, st, mrow0, n0, lane); break;
+    case 2: expert_sums<2, WN, WN_PAD, ROWS>(p, st, mrow0, n0, lane); break;
+    default: expert_sums<1, WN, WN_PAD, ROWS>(p, st, mrow0, n0, lane); break;
   }
 }
 
