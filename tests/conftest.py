@@ -40,3 +40,39 @@ def pytest_sessionfinish(session, exitstatus):
         os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
         with open(path, "w") as f:
             json.dump(_PARITY, f, indent=1)
+
+
+class heartbeat:
+    """Context manager printing a progress line every `every` seconds from a daemon thread (long CPU-oracle phases of
+    a GPU test: the GPU box kills a command that writes nothing for minutes). Use with pytest -s."""
+
+    def __init__(self, what, every=30.0):
+        self.what, self.every = what, every
+
+    def __enter__(self):
+        import threading
+        import time
+        self._stop = threading.Event()
+        t0 = time.time()
+
+        # also appended under gpurun_out/ (the GPU box watches that directory too; pytest captures stdout without -s)
+        log = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "heartbeat.log")
+
+        def run():
+            while not self._stop.wait(self.every):
+                line = f"[{self.what}] {time.time() - t0:.0f} s"
+                print(line, flush=True)
+                try:
+                    os.makedirs(os.path.dirname(log), exist_ok=True)
+                    with open(log, "a") as f:
+                        f.write(line + "\n")
+                except OSError:
+                    pass
+        self._t = threading.Thread(target=run, daemon=True)
+        self._t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._stop.set()
+        self._t.join()
+        return False
