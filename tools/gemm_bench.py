@@ -116,6 +116,26 @@ def main():
             f = lambda: ops.attention(q[:, :C], kv[:, :C], kv[:, C:], n, N_, Nk, 8)  # noqa: E731
         ms = timeit(f, a.iters)
         rows.append((f"attn N={N_} d={d} Nk={Nk}", ms, 4.0 * n * 8 * N_ * Nk * d / ms / 1e9))
+    # HBM-bound glue at the bench's shapes (GB/s = algorithmic bytes / time): GroupNorm statistics (read x once),
+    # apply+SiLU (read + write), the one-call groupnorm, LayerNorm (read + write)
+    for H, C in [(64, 320), (64, 640), (32, 640), (32, 1280), (16, 1280), (16, 2560), (8, 1280)]:
+        x = torch.randn(n * H * H, C, device=dev).half()
+        gm, bt = torch.randn(C, device=dev).half(), torch.randn(C, device=dev).half()
+        byt = n * H * H * C * 2
+        ms = timeit(lambda: ops.groupnorm_stats(x, n, H * H, gm, bt, 1e-5), a.iters)
+        rows.append((f"gn-stats {H}x{H} C={C} (GB/s)", ms, byt / ms / 1e6))
+        sc, sh = ops.groupnorm_stats(x, n, H * H, gm, bt, 1e-5)
+        y = torch.empty_like(x)
+        ms = timeit(lambda: ops.groupnorm_apply(x, n, H * H, sc, sh, True, out=y), a.iters)
+        rows.append((f"gn-apply {H}x{H} C={C} (GB/s)", ms, 2 * byt / ms / 1e6))
+        ms = timeit(lambda: ops.groupnorm(x, n, H * H, gm, bt, 1e-5, silu=True, out=y), a.iters)
+        rows.append((f"groupnorm {H}x{H} C={C} (GB/s)", ms, 3 * byt / ms / 1e6))
+    for M, C in [(n * 4096, 320), (n * 1024, 640), (n * 256, 1280), (n * 64, 1280)]:
+        x = torch.randn(M, C, device=dev).half()
+        gm, bt = torch.randn(C, device=dev).half(), torch.randn(C, device=dev).half()
+        y = torch.empty_like(x)
+        ms = timeit(lambda: ops.layernorm(x, gm, bt, 1e-5, out=y), a.iters)
+        rows.append((f"layernorm M={M} C={C} (GB/s)", ms, 2 * M * C * 2 / ms / 1e6))
     for name, ms, tf in rows:
         if a.only and a.only not in name:
             continue
