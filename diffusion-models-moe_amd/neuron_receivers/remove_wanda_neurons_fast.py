@@ -15,6 +15,12 @@ its columns permuted into the experts' neuron order (converted once per (t, l, l
 top-k keep bits, in one sdmoe_linear_masked launch, and advances the counter exactly as linear_hook_fn does.
 The GEGLU variant hook_fn (:31-61, mask over the gate half of proj.weight) uses the same bitmask path, and so does
 the text-encoder variant text_hook_fn (:85-101, hook_module='text': mask M[0][l] over CLIPMLP.fc2).
+Baked masked weights (the U-Net ff.net.2 hooks): the masks are the same for every prompt batch, so W * (1 - M[t][l])
+is materialised ONCE per (t, l) (and routing order) into an HBM cache (bake_budget_bytes, default 24 GiB: all 50 x 16
+masked SD-1.4 down projections are ~5 GB of the 288 GB) and the per-call GEMM is then the plain (or keep-masked)
+one. In-GEMM masking re-applies the mask in every row tile -- 256 times per call at 64x64 -- and measured 156 us
+against 86 us for the keep-only GEMM at M = 65536 (profiles/r02_rocprof_summary_union.txt); the two are
+bit-identical (tests/test_gpu_wanda.py). Past the budget, or with bake_budget_bytes = 0, the in-GEMM path runs.
 """
 from __future__ import annotations
 
@@ -48,6 +54,7 @@ class WandaRemoveNeuronsFast(NeuronPredictivity):
         self.layer = 0
         self.gates = []
         self._dev = {}
+        self._baked_bytes = 0
 
     @classmethod
     def from_packed(cls, seed, packed, T, n_layers, **kw):
@@ -58,7 +65,10 @@ class WandaRemoveNeuronsFast(NeuronPredictivity):
         obj.remove_timesteps, obj.weights_shape = None, None
         obj.mask_bits = {t: {l: np.asarray(packed[t][l], dtype=np.uint8) for l in range(n_layers)} for t in range(T)}
         obj.timestep, obj.layer, obj.gates, obj._dev = 0, 0, [], {}
+        obj._baked_bytes = 0
         return obj
+
+    bake_budget_bytes = 24 << 30  # HBM for baked masked weights (class default; 0 = always mask inside the GEMM)
 
     def dense_mask(self, t, l):
         bits = self.mask_bits[t][l]
@@ -68,6 +78,8 @@ class WandaRemoveNeuronsFast(NeuronPredictivity):
         self.mask_bits[t][l] = np.asarray(bits, dtype=np.uint8)
         # drop the device copy and every layout derived from it (K-major, permuted, GEGLU gate-half forms)
         for key in [k for k in self._dev if k == (t, l) or (isinstance(k[0], str) and tuple(k[1:3]) == (t, l))]:
+            if key[0] == "baked":
+                self._baked_bytes -= self._dev[key].numel() * 2
             del self._dev[key]
 
     def device_bits(self, t, l, device):
@@ -85,6 +97,22 @@ class WandaRemoveNeuronsFast(NeuronPredictivity):
             d = self._dev[key] = ops.wmask_kmajor(self.device_bits(t, l, device), perm)
         return d
 
+    def baked_weight(self, t, l, weight, perm=None):
+        """W * (1 - M[t][l]) (columns reordered by perm, int32 device [4C], if given), made once per (t, l, weight
+        version, perm) with sdmoe_mask_weight and kept in HBM; None when it would exceed bake_budget_bytes."""
+        key = ("baked", t, l, weight.data_ptr(), weight._version, None if perm is None else perm.data_ptr())
+        w = self._dev.get(key)
+        if w is None:
+            nbytes = weight.numel() * weight.element_size()
+            if self._baked_bytes + nbytes > self.bake_budget_bytes:
+                return None
+            w = ops.mask_weight(weight, self.device_bits(t, l, weight.device))
+            if perm is not None:
+                w = torch.index_select(w, 1, perm.long()).contiguous()
+            self._dev[key] = w
+            self._baked_bytes += nbytes
+        return w
+
     def _check_shape(self, bits, weight, what):
         if bits.shape[0] != weight.shape[0] or bits.shape[1] * 8 != weight.shape[1]:
             raise ValueError(f"{what} mask ({self.timestep},{self.layer}) shape {tuple(bits.shape)} does not match "
@@ -96,8 +124,12 @@ class WandaRemoveNeuronsFast(NeuronPredictivity):
         ff.net.2's weight with its columns in that order. Returns y + residual; advances the (t, l) counter."""
         bits = self.device_bits(self.timestep, self.layer, module.weight.device)
         self._check_shape(bits, module.weight, "ff.net.2")
-        wm = self.device_kmajor(self.timestep, self.layer, module.weight.device, perm)
-        y = ops.linear_masked(x2d, weight_perm, module.bias, keep=keep, wmask=wm, residual=residual)
+        wb = self.baked_weight(self.timestep, self.layer, module.weight.data, perm)
+        if wb is not None:
+            y = ops.linear_masked(x2d, wb, module.bias, keep=keep, residual=residual)
+        else:
+            wm = self.device_kmajor(self.timestep, self.layer, module.weight.device, perm)
+            y = ops.linear_masked(x2d, weight_perm, module.bias, keep=keep, wmask=wm, residual=residual)
         self.update_time_layer()
         return y
 
@@ -127,7 +159,11 @@ class WandaRemoveNeuronsFast(NeuronPredictivity):
         x = input[0]
         bits = self.device_bits(self.timestep, self.layer, module.weight.device)
         self._check_shape(bits, module.weight, "ff.net.2")
-        y = module.run(x.reshape(-1, x.shape[-1]), wmask=self.device_kmajor(self.timestep, self.layer, bits.device))
+        wb = self.baked_weight(self.timestep, self.layer, module.weight.data)
+        if wb is not None:
+            y = module.run(x.reshape(-1, x.shape[-1]), weight=wb)
+        else:
+            y = module.run(x.reshape(-1, x.shape[-1]), wmask=self.device_kmajor(self.timestep, self.layer, bits.device))
         self.update_time_layer()
         return y.view(*x.shape[:-1], module.weight.shape[0])
 

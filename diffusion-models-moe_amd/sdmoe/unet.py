@@ -52,8 +52,9 @@ class LoRACompatibleLinear(nn.Module):
     def out_features(self):
         return self.weight.shape[0]
 
-    def run(self, x2d, **kw):
-        return ops.linear(x2d, self.weight, self.bias, **kw)
+    def run(self, x2d, weight=None, **kw):
+        """y = x2d @ W^T + b (W = self.weight unless a stand-in of the same shape is given, e.g. a baked masked copy)."""
+        return ops.linear(x2d, self.weight if weight is None else weight, self.bias, **kw)
 
     def forward(self, x, scale=1.0):
         if self._sdmoe_deferred and self._forward_hooks:

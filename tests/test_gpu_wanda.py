@@ -77,9 +77,11 @@ def test_wmask_kmajor_layout_and_permutation():
 
 
 @pytest.mark.parametrize("dtype", ["float16"])
-def test_wanda_hook_on_reference_fixture(dtype, parity_report):
+@pytest.mark.parametrize("bake", [True, False], ids=["baked", "in_gemm"])
+def test_wanda_hook_on_reference_fixture(dtype, bake, parity_report):
     """The HIP Wanda hook, driven like the reference (counter over the 5 layers of t = 0), on the masks of the
-    reference's weights_320_1280.csv, vs the reference hook's own outputs."""
+    reference's weights_320_1280.csv, vs the reference hook's own outputs -- with the baked masked weights (default)
+    and with the mask applied inside the GEMM (bake_budget_bytes = 0)."""
     from neuron_receivers import WandaRemoveNeuronsFast
     from sdmoe.unet import LoRACompatibleLinear
     with np.load(os.path.join(GOLD, f"wanda_320x1280_{dtype}.npz"), allow_pickle=False) as z:
@@ -87,6 +89,8 @@ def test_wanda_hook_on_reference_fixture(dtype, parity_report):
     bits = c["mask_bits"]  # [L, 320, 160]
     L = bits.shape[0]
     rec = WandaRemoveNeuronsFast.from_packed(0, {0: {l: bits[l] for l in range(L)}}, 1, L, store_gates=False)
+    if not bake:
+        rec.bake_budget_bytes = 0
     w, b = synth.down_weights(320, int(c["w_seed"]))
     lin = LoRACompatibleLinear(torch.from_numpy(w).half().to(DEV), torch.from_numpy(b).half().to(DEV))
     x = torch.from_numpy(c["x"]).to(DEV)
@@ -105,10 +109,12 @@ def test_wanda_hook_on_reference_fixture(dtype, parity_report):
         y0 = ops.linear(x.reshape(-1, 1280), lin.weight, lin.bias).float().cpu().numpy().reshape(y.shape)
         assert np.abs(y0 - ref).max() > 10 * np.abs(y - ref).max()
     assert (rec.timestep, rec.layer) == (1, 0)
-    parity_report(f"wanda_hook_fixture[{dtype}]", layers=L, max_ulps=worst)
+    assert any(isinstance(k[0], str) and k[0] == ("baked" if bake else "kmajor") for k in rec._dev)
+    parity_report(f"wanda_hook_fixture[{dtype},{'baked' if bake else 'in_gemm'}]", layers=L, max_ulps=worst)
 
 
-def test_union_wanda_moe_pipeline_sd14(parity_report):
+@pytest.mark.parametrize("bake", [True, False], ids=["baked", "in_gemm"])
+def test_union_wanda_moe_pipeline_sd14(bake, parity_report):
     """Config 4's per-GPU path at SD-1.4 widths (32x32 latents, 2 prompts, 2 DDIM steps): a two-concept union Wanda
     mask on every ff.net.2 together with RemoveExperts routing (relufied, top-k 0.2, removal for t < 20). The
     FeedForward keeps the fused routed path (union mask permuted with the experts, one sdmoe_linear_masked launch
@@ -144,6 +150,8 @@ def test_union_wanda_moe_pipeline_sd14(parity_report):
     mc.handle_multiple_concepts(list(concepts))
     union = {t: {l: H.union_masks([concepts[c][t][l] for c in concepts]) for l in range(L)} for t in range(T)}
     wanda = mc.union_neuron_remover
+    if not bake:
+        wanda.bake_budget_bytes = 0
     g = torch.Generator().manual_seed(24)
     lists = {t: {l: sorted(torch.randperm(layers[l][1], generator=g)[:layers[l][1] // 10].tolist())
                  for l in range(L)} for t in range(T)}
@@ -160,7 +168,10 @@ def test_union_wanda_moe_pipeline_sd14(parity_report):
     torch.cuda.synchronize()
     assert (wanda.timestep, wanda.layer) == (2, 0) and (rec.timestep, rec.layer) == (2, 0)
     assert all(m._out_keep is not None for m in mods), "fused routed path did not run under the Wanda hook"
-    assert any(k[0] == "kmajor" and k[3] is not None for k in wanda._dev if isinstance(k[0], str))
+    if bake:  # the masked weight baked once per (t, l) in the experts' column order
+        assert any(k[0] == "baked" and k[5] is not None for k in wanda._dev if isinstance(k[0], str))
+    else:     # the mask's permuted K-major form applied inside the GEMM
+        assert any(k[0] == "kmajor" and k[3] is not None for k in wanda._dev if isinstance(k[0], str))
     got = torch.stack(out).float().cpu()
     ref = UNetRef({k: v.half().float() for k, v in sd.items()}, cfg)
 
@@ -171,7 +182,7 @@ def test_union_wanda_moe_pipeline_sd14(parity_report):
     stats = dict(rows=0, clear=0, clear_mismatch=0, forced=0)
     exp = run_oracle(ref, cfg, prompts, 2, ff_hook_factory=forced_factory(layers, "relu", rec.sels, lists, stats),
                      down_hook_factory=down_factory)
-    parity_report("pipeline_sd14_32x32_union_wanda_moe", rows=stats["rows"], clear=stats["clear"],
+    parity_report(f"pipeline_sd14_32x32_union_wanda_moe[{'baked' if bake else 'in_gemm'}]", rows=stats["rows"], clear=stats["clear"],
                   near_tie=stats["rows"] - stats["clear"], flips=stats["forced"], rel_l2=rel_l2(got, exp))
     assert stats["clear_mismatch"] == 0, stats
     assert rel_l2(got, exp) <= 1e-2
