@@ -58,6 +58,9 @@ def parse():
     p.add_argument("--no-roofline", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-evals", type=int, default=2, help="CPU oracle U-Net evaluations to time")
+    p.add_argument("--cpu-full-image", action="store_true",
+                   help="cpu_baseline: time one whole image (all inference steps of the oracle's DDIM+CFG loop, "
+                        "several minutes) instead of the bounded cpu-evals sample")
     p.add_argument("--traffic", type=str, default=os.path.join(ROOT, "profiles", "pmc_conv_traffic.json"),
                    help="PMC summary json from tools/pmc_traffic.py (HBM bytes per conv launch)")
     return p.parse_args()
@@ -234,6 +237,20 @@ def cpu_baseline(args):
 
     x = torch.randn(2, 4, 64, 64)
     ctx = torch.stack([prompt_embedding("", 768), prompt_embedding("a painting", 768)])
+    if args.cpu_full_image:  # one measured image: the oracle's whole DDIM + CFG loop
+        from oracle.unet_ref import denoise
+
+        def factory(step):
+            print(f"[cpu_baseline] step {step}", file=sys.stderr, flush=True)
+            return hook
+        with torch.no_grad():
+            ref(x, 981.0, ctx, ff_hook=hook)  # warm-up (allocator, threads)
+            t0 = time.perf_counter()
+            denoise(ref, x[:1], ctx[:1], ctx[1:], num_inference_steps=args.inference_steps, ff_hook_factory=factory)
+            per_image = time.perf_counter() - t0
+        return {"value": 1.0 / per_image, "unit": "images/s", "cores": threads, "kind": "port",
+                "sample": f"one whole image measured: {args.inference_steps} DDIM steps x CFG U-Net eval (B=1, "
+                          f"2x4x64x64, MoE routing + removal hooks) in {per_image:.1f} s"}
     with torch.no_grad():
         ref(x, 981.0, ctx, ff_hook=hook)  # warm-up (allocator, threads)
         t0 = time.perf_counter()
