@@ -135,9 +135,13 @@ def recording(cls):
     return Rec
 
 
-def forced_factory(layers, act, sels, removed=None, stats=None):
+def forced_factory(layers, act, sels, removed=None, stats=None, margin=16):
     """Oracle hook (fp16 arithmetic, as in the reference's fp16 pipeline) that checks its own top-k against
-    the device's on every row clear of an fp16 near-tie, then uses the device's selection (teacher forcing)."""
+    the device's on every row clear of an fp16 near-tie, then uses the device's selection (teacher forcing).
+    A row is clear when its k-th/(k+1)-th score gap exceeds `margin` fp16 ulps: the hook's INPUT comes from the
+    oracle's fp32 trunk while the device's comes from its fp16 trunk, so the margin has to cover the trunk's
+    propagated rounding noise (deeper stacks need more); stats["max_mismatch_gap_ulps"] records the largest gap of
+    any row whose selections differ."""
     import numpy as np
 
     def factory(step):
@@ -150,9 +154,13 @@ def forced_factory(layers, act, sels, removed=None, stats=None):
             dev_sel = sels[step * len(layers) + layer]
             s = np.sort(score.float().numpy(), axis=1)[:, ::-1]
             gap = s[:, k - 1] - s[:, k] if k < E else np.full(s.shape[0], np.inf)
-            clear = gap > 16 * np.spacing(np.abs(s[:, min(k, E - 1)]).astype(np.float16)).astype(np.float32)
+            ulp = np.spacing(np.abs(s[:, min(k, E - 1)]).astype(np.float16)).astype(np.float32)
+            clear = gap > margin * ulp
             mism = (sel_o.numpy() != dev_sel.numpy()).any(1)
             if stats is not None:
+                if mism.any():
+                    g = float(np.max(gap[mism] / ulp[mism]))
+                    stats["max_mismatch_gap_ulps"] = max(stats.get("max_mismatch_gap_ulps", 0.0), g)
                 stats["rows"] += clear.size
                 stats["clear"] += int(clear.sum())
                 stats["clear_mismatch"] += int((mism & clear).sum())
