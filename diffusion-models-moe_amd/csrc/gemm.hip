@@ -255,11 +255,18 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
   constexpr int KEEP_OFF = STAGE_AB + (PADDED ? 1024 : 0);
   constexpr int WKEEP_OFF = KEEP_OFF + keep_a_bytes<BM, MODE>();
   constexpr int STAGE = KEEP_OFF + keep_stage_bytes<BM, BN, MODE>();
+  // epilogue staging: fp16 final values (row stride RS16 halves: 16-B aligned rows, conflict-free b64 stores of the
+  // swapped fragments) in NPASS16 passes; the fp32 path (GEGLU, activation, residual) in NPASS passes
+  constexpr int RS16 = WN + 8;
+  constexpr int NPASS16 = (NW * WM * RS16 * 2 <= NSTAGE * STAGE) ? 1 : (NW * (WM / 2) * RS16 * 2 <= NSTAGE * STAGE) ? 2
+                          : ((NW * (WM / 4) * RS16 * 2 <= NSTAGE * STAGE) ? 4 : 8);
   constexpr int WN_PAD = WN + 4;
   constexpr int NPASS = (NW * (WM / 2) * WN_PAD * 4 <= NSTAGE * STAGE) ? 2 : ((NW * (WM / 4) * WN_PAD * 4 <= NSTAGE * STAGE) ? 4 : 8);
-  static_assert(FM % NPASS == 0, "epilogue passes must split the wave's fragment rows");
+  static_assert(FM % NPASS == 0 && FM % NPASS16 == 0, "epilogue passes must split the wave's fragment rows");
   constexpr int EPI = NW * (WM / NPASS) * WN_PAD * 4;
-  constexpr int SMEM0 = (NSTAGE * STAGE > EPI) ? NSTAGE * STAGE : EPI;
+  constexpr int EPI16 = NW * (WM / NPASS16) * RS16 * 2;
+  constexpr int SMEM0 = (NSTAGE * STAGE > EPI) ? (NSTAGE * STAGE > EPI16 ? NSTAGE * STAGE : EPI16)
+                                              : (EPI > EPI16 ? EPI : EPI16);
   constexpr int LUT_OFF = SMEM0;                 // MODE_KEEP: 16-entry nibble -> lane-mask table behind everything
   constexpr int SMEM = SMEM0 + (KEEP ? KEEP_LUT_BYTES : 0);
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
@@ -391,6 +398,11 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
     if constexpr (KEEP) bld16(rsK, sa + kdst, kvoff, (unsigned)ks * kstride);
   };
 
+  // SWAP: C^T fragments (the MFMA's operands swapped): acc[i][j][r] = C[row wr*WM + 16 i + fr][col wc*WN + 16 j +
+  // 4 fg + r], 4 consecutive output columns of one row per lane, so the epilogue works on half4 / float4 row pieces.
+  // The routed GEGLU keeps C fragments (rows 16 i + 4 fg + r, column 16 j + fr): its epilogue measured 6 % slower
+  // on the swapped layout.
+  constexpr bool SWAP = !GEGLU;
   float4v acc[FM][FN];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -480,9 +492,12 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
           }
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-          for (int j = 0; j < FN; ++j) acc[2 * g][j] = mfma16x16x32(a0, bcur[j], acc[2 * g][j]);
+          for (int j = 0; j < FN; ++j)
+            acc[2 * g][j] = SWAP ? mfma16x16x32(bcur[j], a0, acc[2 * g][j]) : mfma16x16x32(a0, bcur[j], acc[2 * g][j]);
 #pragma unroll
-          for (int j = 0; j < FN; ++j) acc[2 * g + 1][j] = mfma16x16x32(a1, bcur[j], acc[2 * g + 1][j]);
+          for (int j = 0; j < FN; ++j)
+            acc[2 * g + 1][j] = SWAP ? mfma16x16x32(bcur[j], a1, acc[2 * g + 1][j])
+                                     : mfma16x16x32(a1, bcur[j], acc[2 * g + 1][j]);
           __builtin_amdgcn_sched_barrier(0);
           a0 = n0;
           a1 = n1;
@@ -503,14 +518,14 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
-          for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32(af[i], bf[j], acc[i][j]);
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = SWAP ? mfma16x16x32(bf[j], af[i], acc[i][j]) : mfma16x16x32(af[i], bf[j], acc[i][j]);
       }
     }
     if (p.prio) __builtin_amdgcn_s_setprio(0);
   }
 
-  // ---- epilogue: per wave, stage half of its fp32 tile (FM/2 fragment rows) in LDS at a time, then write
-  // 8-column chunks with 16-B (fp16) / 32-B (fp32 split-K slab) stores
+  // ---- epilogue
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (p.diag & 4) {  // diagnostics: keep the accumulators live, store nothing
 #pragma unroll
@@ -519,43 +534,112 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
       for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(acc[i][j]));
     return;
   }
+  const int mw = m0 + wr * WM, nw = n0 + wc * WN;  // this wave's output tile origin
+  if (SWAP && p.part) {  // split-K: fp32 partial slab [split][M][N], 16-B stores straight from the accumulators
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int m = mw + 16 * i + fr, n = nw + 16 * j + 4 * fg;
+        if (m < p.M && n < p.N) *reinterpret_cast<float4v*>(p.part + ((long)split * p.M + m) * p.N + n) = acc[i][j];
+      }
+    return;
+  }
   __syncthreads();
+  constexpr int CPR = WN / 8;
+  if (!GEGLU && p.act == ACT_NONE && !p.R) {
+    // fp16 path: bias and per-image column add in registers on each lane's 4-column row piece (one rounding, as
+    // epilogue8), staged as fp16 (one ds_write_b64 per fragment: 1/2.5 of the LDS time of staging fp32 with 4
+    // ds_write_b32), then copied out in 16-B row chunks: 175 -> 166 us for the M = 65536, N = 2560, K = 320 linear,
+    // 1-3 % on the convs. Measured slower and therefore not used: residual loads in registers (8-B pieces of 16
+    // rows: 29 -> 33 us for linear+res at 64x64) and the GEGLU epilogue on fp16 staging (170 -> 179 us); an
+    // activation's code keeps the unrolled fragment loop from unrolling (acc then lives in scratch).
+    half4 b4[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = nw + 16 * j + 4 * fg;
+      b4[j] = (p.bias && n < p.N) ? *reinterpret_cast<const half4*>(p.bias + n) : (half4){0, 0, 0, 0};
+    }
+    half_t* st = reinterpret_cast<half_t*>(smem) + wave * (WM / NPASS16) * RS16;
+#pragma unroll
+    for (int h = 0; h < NPASS16; ++h) {
+#pragma unroll
+      for (int i = 0; i < FM / NPASS16; ++i) {
+        // one fragment row at a time: keeps the hoisted bias / column-add / residual loads to FN pieces (the 8-wave
+        // 256x320 tiles hold 160 accumulator VGPRs here and spilled when the compiler hoisted all of them)
+        __builtin_amdgcn_sched_barrier(0);
+        const int m = mw + 16 * (h * (FM / NPASS16) + i) + fr;
+        const half_t* cap = (p.coladd && m < p.M) ? p.coladd + (long)(m / p.rows_per_batch) * p.coladd_bstride : nullptr;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int n = nw + 16 * j + 4 * fg;
+          float4v v = acc[h * (FM / NPASS16) + i][j];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += (float)b4[j][r];
+          if (cap && n < p.N) {
+            const half4 c = *reinterpret_cast<const half4*>(cap + n);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += (float)c[r];
+          }
+          half4 y;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) y[r] = (half_t)v[r];
+          *reinterpret_cast<half4*>(st + (16 * i + fr) * RS16 + 16 * j + 4 * fg) = y;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      for (int id = lane; id < (WM / NPASS16) * CPR; id += 64) {
+        const int r = id / CPR, c8 = id - r * CPR;
+        const int m = mw + h * (WM / NPASS16) + r, n = nw + c8 * 8;
+        if (m >= p.M || n >= p.N) continue;
+        const half8 o = *reinterpret_cast<const half8*>(st + r * RS16 + c8 * 8);
+        if (p.diag & 8) asm volatile("" ::"v"(o));
+        else *reinterpret_cast<half8*>(p.C + (long)m * p.ldc + n) = o;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    return;
+  }
+  // fp32 path (GEGLU, activation, residual): stage the raw accumulators (one b128 per fragment), then the routed
+  // GEGLU pass or epilogue8 on 8-column row chunks
   float* st = reinterpret_cast<float*>(smem) + wave * (WM / NPASS) * WN_PAD;
   // GEGLU: this wave's WN bias values (fp32) copied once into LDS past the staging area (per wave, no block sync)
   float* gbias = reinterpret_cast<float*>(smem + EPI) + wave * WN;
   if constexpr (GEGLU) {
     static_assert(EPI + NW * WN * 4 <= SMEM, "GEGLU bias slot must fit behind the epilogue staging");
-    for (int c = lane; c < WN; c += 64) gbias[c] = (float)p.bias[n0 + wc * WN + c];
+    for (int c = lane; c < WN; c += 64) gbias[c] = (float)p.bias[nw + c];
   }
-  constexpr int CPR = WN / 8;
 #pragma unroll
   for (int h = 0; h < NPASS; ++h) {
 #pragma unroll
     for (int i = 0; i < FM / NPASS; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
+      for (int j = 0; j < FN; ++j) {
+        if constexpr (SWAP) {
+          *reinterpret_cast<float4v*>(st + (16 * i + fr) * WN_PAD + 16 * j + 4 * fg) = acc[h * (FM / NPASS) + i][j];
+        } else {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) st[(i * 16 + fg * 4 + r) * WN_PAD + j * 16 + fr] = acc[h * (FM / NPASS) + i][j][r];
+          for (int r = 0; r < 4; ++r) st[(16 * i + 4 * fg + r) * WN_PAD + 16 * j + fr] = acc[h * (FM / NPASS) + i][j][r];
+        }
+      }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if constexpr (GEGLU) {
-      geglu_pass<WN, WN_PAD, WM / NPASS>(p, st, m0 + wr * WM + h * (WM / NPASS), n0 + wc * WN, lane, gbias);
+      geglu_pass<WN, WN_PAD, WM / NPASS>(p, st, mw + h * (WM / NPASS), nw, lane, gbias);
     } else
     for (int id = lane; id < (WM / NPASS) * CPR; id += 64) {
       const int r = id / CPR, c8 = id - r * CPR;
-      const int m = m0 + wr * WM + h * (WM / NPASS) + r, n = n0 + wc * WN + c8 * 8;
+      const int m = mw + h * (WM / NPASS) + r, n = nw + c8 * 8;
       if (m >= p.M || n >= p.N) continue;
       const float* sp = st + r * WN_PAD + c8 * 8;
-      float4v v0 = *reinterpret_cast<const float4v*>(sp), v1 = *reinterpret_cast<const float4v*>(sp + 4);
-      if (p.part) {
-        float* dp = p.part + ((long)split * p.M + m) * p.N + n;
-        *reinterpret_cast<float4v*>(dp) = v0;
-        *reinterpret_cast<float4v*>(dp + 4) = v1;
-      } else {
-        float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-        epilogue8(p, m, n, v);
-      }
+      const float4v v0 = *reinterpret_cast<const float4v*>(sp), v1 = *reinterpret_cast<const float4v*>(sp + 4);
+      float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      epilogue8(p, m, n, v);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
