@@ -751,6 +751,15 @@ int dispatch(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
   if ((MODE == MODE_GEMM || MODE >= MODE_KEEP) && p.N % 160 == 0 && nt160_128 >= 200 && nt160_128 < 320 &&
       p.K <= 5120)
     return launch_tile<64, 160, 2, 2, MODE>(p, ws, ws_floats, s);
+  // convs (tools/gemm_bench.py --tile/--stages sweep, same box): the 16x16-level 3x3 convs (M = 4096, N = 1280,
+  // K = 9 x 1280 / 9 x 2560) on the 8-wave 256x320 tile with a 4-way split-K: 120 / 205 us vs 135 / 237 us on
+  // 256x160 with a 2-way split (the 32x32 level's 1280 -> 640 conv stays on 128x160: 207 vs 221 us); the 64x64 -> 32x32 stride-2 conv (M = 16384, N = 320) on 64x160 tiles at two
+  // workgroups per CU: 38 vs 57 us on 128x160 with a 3-stage ring
+  if constexpr (MODE == MODE_CONV) {
+    if (p.stride == 1 && p.N % 320 == 0 && nt320 < 240 && p.K >= 9 * 1280 && p.M >= 2048 && p.M <= 4096)
+      return launch_tile<256, 320, 2, 4, MODE>(p, ws, ws_floats, s);
+    if (p.stride == 2 && p.N % 160 == 0 && p.M >= 8192) return launch_tile<64, 160, 2, 2, MODE>(p, ws, ws_floats, s);
+  }
   if (p.N % 160 == 0 && p.K >= 2560 && nt160_128 < 300 && !(MODE == MODE_CONV && p.stride == 2))
     return launch_tile<256, 160, 4, 2, MODE>(p, ws, ws_floats, s);
   if (MODE == MODE_CONV_UP) {
