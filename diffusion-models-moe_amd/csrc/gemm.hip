@@ -741,7 +741,9 @@ int dispatch(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
   const int nt160_128 = ((p.M + 127) / 128) * ((p.N + 159) / 160);
   // The keep-masked A operand (routed FFN down projection) takes the 4x2-wave arrangement (wave tile 64x160: half
   // the A fragments to mask per wave): 61 vs 69 us at M = 65536, N = 320, K = 1280 (tools/gemm_bench.py --tile 5).
-  if (p.N % 320 == 0 && nt320 >= 240) {
+  // (180: the 16x16-level fused QKV, M = 4096 x N = 3840 x K = 1280 -- also SDXL's 32x32 level -- 43.8 vs 49.9 us on
+  // 128x160; every other U-Net shape is outside 180..240)
+  if (p.N % 320 == 0 && nt320 >= 180) {
     if constexpr (mode_akeep(MODE)) return launch_tile<256, 320, 4, 2, MODE>(p, ws, ws_floats, s);
     return launch_tile<256, 320, 2, 4, MODE>(p, ws, ws_floats, s);
   }
@@ -753,8 +755,9 @@ int dispatch(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
     return launch_tile<64, 160, 2, 2, MODE>(p, ws, ws_floats, s);
   // convs (tools/gemm_bench.py --tile/--stages sweep, same box): the 16x16-level 3x3 convs (M = 4096, N = 1280,
   // K = 9 x 1280 / 9 x 2560) on the 8-wave 256x320 tile with a 4-way split-K: 120 / 205 us vs 135 / 237 us on
-  // 256x160 with a 2-way split (the 32x32 level's 1280 -> 640 conv stays on 128x160: 207 vs 221 us); the 64x64 -> 32x32 stride-2 conv (M = 16384, N = 320) on 64x160 tiles at two
-  // workgroups per CU: 38 vs 57 us on 128x160 with a 3-stage ring
+  // 256x160 with a 2-way split (the 32x32 level's 1280 -> 640 conv stays on 128x160: 207 vs 221 us); the
+  // 64x64 -> 32x32 stride-2 conv (M = 16384, N = 320) on 64x160 tiles at two workgroups per CU: 38 vs 57 us on
+  // 128x160 with a 3-stage ring
   if constexpr (MODE == MODE_CONV) {
     if (p.stride == 1 && p.N % 320 == 0 && nt320 < 240 && p.K >= 9 * 1280 && p.M >= 2048 && p.M <= 4096)
       return launch_tile<256, 320, 2, 4, MODE>(p, ws, ws_floats, s);

@@ -61,7 +61,8 @@ def main():
         fl = 2.0 * n * OH * OH * Cout * 9 * Cin
         rows.append((f"conv {H}x{H} {Cin}->{Cout} s{st}{' up' if up else ''}", ms, fl / ms / 1e9))
     # linears: (M, N, K)
-    for M, N, K in [(n * 4096, 960, 320), (n * 4096, 2560, 320), (n * 4096, 320, 1280), (n * 4096, 320, 320),
+    for M, N, K in [(n * 4096, 960, 320), (n * 1024, 1920, 640), (n * 256, 3840, 1280), (n * 4096, 320, 320),
+                    (n * 1024, 640, 640), (n * 256, 1280, 1280), (n * 4096, 2560, 320), (n * 4096, 320, 1280),
                     (n * 1024, 5120, 640), (n * 1024, 640, 2560), (n * 256, 10240, 1280), (n * 256, 1280, 5120),
                     (n * 64, 3840, 1280), (n * 77, 2560, 768)]:
         x = torch.randn(M, K, device=dev).half()
