@@ -69,6 +69,12 @@ struct GemmParams {
   // wmask[(k / 64) * N * 8 + n * 8 + (k % 64) / 8] bit (k % 8) SET = W[n, k] removed (zeroed on the B fragments)
   const uint8_t* wmask;
   int wmask_bytes;
+  // LayerNorm folded into the GEMM (MODE_GEMM_LN / MODE_GEGLU_LN): C = rstd_m * (A W'^T - mean_m * wsum) + ln_bias
+  // with W' = W diag(gamma) (fp16), wsum[n] = sum_k W'[n, k], ln_bias[n] = bias[n] + sum_k W[n, k] beta[k] (fp32,
+  // sdmoe_ln_fold); mean_m / rstd_m over the K = C channels of row m, accumulated from the A tiles in LDS
+  const float* ln_wsum;
+  const float* ln_bias;
+  float ln_eps;
 };
 
 SDMOE_DEV int swz(int row) { return (row >> 1) & 7; }
@@ -113,7 +119,9 @@ SDMOE_DEV void epilogue8(const GemmParams& p, int m, int n, float (&v)[8]) {
 
 // GEGLU: GEMM loads, routed-GEGLU epilogue; KEEP: GEMM whose A operand is masked per (row, neuron) by keep bits;
 // WMASK: W operand masked per (row, k) by Wanda bits; KEEPW: both (the routed FFN down projection under a Wanda mask)
-enum { MODE_GEMM = 0, MODE_CONV = 1, MODE_CONV_UP = 2, MODE_GEGLU = 3, MODE_KEEP = 4, MODE_WMASK = 5, MODE_KEEPW = 6 };
+// GEMM_LN / GEGLU_LN: GEMM / GEGLU with the LayerNorm of the A rows folded in (row statistics from the A tiles)
+enum { MODE_GEMM = 0, MODE_CONV = 1, MODE_CONV_UP = 2, MODE_GEGLU = 3, MODE_KEEP = 4, MODE_WMASK = 5, MODE_KEEPW = 6,
+       MODE_GEMM_LN = 7, MODE_GEGLU_LN = 8 };
 constexpr bool mode_akeep(int mode) { return mode == MODE_KEEP || mode == MODE_KEEPW; }
 constexpr bool mode_wmask(int mode) { return mode == MODE_WMASK || mode == MODE_KEEPW; }
 
@@ -235,7 +243,8 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
   constexpr int RPP = 1024 / RB;                 // rows per 1-KiB LDS-DMA piece
   auto swzk = [](int row) { return (row >> 1) & (CPRW - 1); };  // conflict-free b128 fragment reads
   constexpr bool CONV = MODE == MODE_CONV || MODE == MODE_CONV_UP;
-  constexpr bool GEGLU = MODE == MODE_GEGLU;
+  constexpr bool GEGLU = MODE == MODE_GEGLU || MODE == MODE_GEGLU_LN;
+  constexpr bool LN = MODE == MODE_GEMM_LN || MODE == MODE_GEGLU_LN;
   constexpr bool AKEEP = mode_akeep(MODE), WKEEP = mode_wmask(MODE);
   constexpr bool KEEP = AKEEP || WKEEP;
   static_assert(!KEEP || BKT == 64, "keep bytes are laid out per 64-deep K-step");
@@ -268,8 +277,19 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
   constexpr int SMEM0 = (NSTAGE * STAGE > EPI) ? (NSTAGE * STAGE > EPI16 ? NSTAGE * STAGE : EPI16)
                                               : (EPI > EPI16 ? EPI : EPI16);
   constexpr int LUT_OFF = SMEM0;                 // MODE_KEEP: 16-entry nibble -> lane-mask table behind everything
-  constexpr int SMEM = SMEM0 + (KEEP ? KEEP_LUT_BYTES : 0);
+  constexpr int SMEM1 = SMEM0 + (KEEP ? KEEP_LUT_BYTES : 0);
+  // LN: per tile row (rstd, -mean*rstd), then the tile's BN columns of wsum and ln_bias (fp32), behind everything
+  constexpr int LN_ROW_OFF = SMEM1, LN_COL_OFF = SMEM1 + BM * 8;
+  constexpr int SMEM = SMEM1 + (LN ? BM * 8 + BN * 8 : 0);
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+  constexpr int NT = 64 * NW;
+  // LN row statistics: lane tid reads 16-B chunk (tid % 8) of tile rows tid / 8 + (NT / 8) t, t < LN_IPL, every
+  // K-step (8 lanes cover one 128-B row: conflict-free), summing x and x^2 with v_dot2_f32_f16
+  constexpr int LN_IPL = LN ? (BM * 8) / NT : 1;
+  static_assert(!LN || ((BM * 8) % NT == 0 && BK == 64), "LN statistics: whole 16-B chunks per lane");
+  float ln_s1[LN_IPL], ln_s2[LN_IPL];
+#pragma unroll
+  for (int t = 0; t < LN_IPL; ++t) ln_s1[t] = ln_s2[t] = 0.f;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -522,6 +542,21 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
             acc[i][j] = SWAP ? mfma16x16x32(bf[j], af[i], acc[i][j]) : mfma16x16x32(af[i], bf[j], acc[i][j]);
       }
     }
+    if constexpr (LN) {
+      typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+      const h2 one2 = {(half_t)1.f, (half_t)1.f};
+#pragma unroll
+      for (int t = 0; t < LN_IPL; ++t) {
+        const int row = tid / 8 + (NT / 8) * t, ch = tid & 7;
+        const half8 x = *reinterpret_cast<const half8*>(sa + row * RB + ((ch ^ swzk(row)) << 4));
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const h2 x2 = {x[2 * q], x[2 * q + 1]};
+          ln_s1[t] = __builtin_amdgcn_fdot2(x2, one2, ln_s1[t], false);
+          ln_s2[t] = __builtin_amdgcn_fdot2(x2, x2, ln_s2[t], false);
+        }
+      }
+    }
     if (p.prio) __builtin_amdgcn_s_setprio(0);
   }
 
@@ -545,6 +580,31 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
       }
     return;
   }
+  float* ln_row = reinterpret_cast<float*>(smem + LN_ROW_OFF);  // [BM][2]: rstd, -mean * rstd
+  float* ln_col = reinterpret_cast<float*>(smem + LN_COL_OFF);  // [BN] wsum, then [BN] ln_bias
+  if constexpr (LN) {
+#pragma unroll
+    for (int t = 0; t < LN_IPL; ++t) {
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) {
+        ln_s1[t] += __shfl_xor(ln_s1[t], o, 64);
+        ln_s2[t] += __shfl_xor(ln_s2[t], o, 64);
+      }
+      if ((tid & 7) == 0) {
+        const int row = tid / 8 + (NT / 8) * t;
+        const float mean = ln_s1[t] / (float)p.K;
+        const float var = fmaxf(ln_s2[t] / (float)p.K - mean * mean, 0.f);
+        const float rstd = rsqrtf(var + p.ln_eps);
+        ln_row[2 * row] = rstd;
+        ln_row[2 * row + 1] = -mean * rstd;
+      }
+    }
+    for (int c = tid; c < BN; c += NT) {
+      const bool ok = n0 + c < p.N;
+      ln_col[c] = ok ? p.ln_wsum[n0 + c] : 0.f;
+      ln_col[BN + c] = ok ? p.ln_bias[n0 + c] : 0.f;
+    }
+  }
   __syncthreads();
   constexpr int CPR = WN / 8;
   if (!GEGLU && p.act == ACT_NONE && !p.R) {
@@ -558,7 +618,7 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int n = nw + 16 * j + 4 * fg;
-      b4[j] = (p.bias && n < p.N) ? *reinterpret_cast<const half4*>(p.bias + n) : (half4){0, 0, 0, 0};
+      b4[j] = (!LN && p.bias && n < p.N) ? *reinterpret_cast<const half4*>(p.bias + n) : (half4){0, 0, 0, 0};
     }
     half_t* st = reinterpret_cast<half_t*>(smem) + wave * (WM / NPASS16) * RS16;
 #pragma unroll
@@ -570,10 +630,23 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
         __builtin_amdgcn_sched_barrier(0);
         const int m = mw + 16 * (h * (FM / NPASS16) + i) + fr;
         const half_t* cap = (p.coladd && m < p.M) ? p.coladd + (long)(m / p.rows_per_batch) * p.coladd_bstride : nullptr;
+        float a = 0.f, c = 0.f;  // LN: this lane's row (rstd, -mean * rstd), read once per fragment row
+        if constexpr (LN) {
+          const int rl = wr * WM + 16 * (h * (FM / NPASS16) + i) + fr;
+          a = ln_row[2 * rl];
+          c = ln_row[2 * rl + 1];
+        }
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
           const int n = nw + 16 * j + 4 * fg;
           float4v v = acc[h * (FM / NPASS16) + i][j];
+          if constexpr (LN) {  // rstd * (acc - mean * wsum) + ln_bias
+            const int cl = wc * WN + 16 * j + 4 * fg;
+            const float4v ws = *reinterpret_cast<const float4v*>(ln_col + cl);
+            const float4v lb = *reinterpret_cast<const float4v*>(ln_col + BN + cl);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = __builtin_fmaf(a, v[r], __builtin_fmaf(c, ws[r], lb[r]));
+          }
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] += (float)b4[j][r];
           if (cap && n < p.N) {
@@ -610,22 +683,41 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
   // GEGLU: this wave's WN bias values (fp32) copied once into LDS past the staging area (per wave, no block sync)
   float* gbias = reinterpret_cast<float*>(smem + EPI) + wave * WN;
   if constexpr (GEGLU) {
-    static_assert(EPI + NW * WN * 4 <= SMEM, "GEGLU bias slot must fit behind the epilogue staging");
-    for (int c = lane; c < WN; c += 64) gbias[c] = (float)p.bias[nw + c];
+    static_assert(EPI + NW * WN * 4 <= SMEM1, "GEGLU bias slot must fit behind the epilogue staging");
+    for (int c = lane; c < WN; c += 64) gbias[c] = LN ? p.ln_bias[nw + c] : (float)p.bias[nw + c];
+  }
+  float lnws[LN ? FN : 1];  // GEGLU LN: wsum of this lane's column in each fragment (C layout: column 16 j + fr)
+  if constexpr (LN && !SWAP) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) lnws[j] = ln_col[wc * WN + 16 * j + fr];
   }
 #pragma unroll
   for (int h = 0; h < NPASS; ++h) {
 #pragma unroll
-    for (int i = 0; i < FM / NPASS; ++i)
+    for (int i = 0; i < FM / NPASS; ++i) {
+      float4v lra = {0, 0, 0, 0}, lrc = {0, 0, 0, 0};  // GEGLU LN: (rstd, -mean*rstd) of rows 4 fg .. 4 fg + 3
+      if constexpr (LN && !SWAP) {
+        const int rl = wr * WM + 16 * (h * (FM / NPASS) + i) + 4 * fg;
+        const float4v r01 = *reinterpret_cast<const float4v*>(ln_row + 2 * rl);
+        const float4v r23 = *reinterpret_cast<const float4v*>(ln_row + 2 * rl + 4);
+        lra = (float4v){r01[0], r01[2], r23[0], r23[2]};
+        lrc = (float4v){r01[1], r01[3], r23[1], r23[3]};
+      }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         if constexpr (SWAP) {
           *reinterpret_cast<float4v*>(st + (16 * i + fr) * WN_PAD + 16 * j + 4 * fg) = acc[h * (FM / NPASS) + i][j];
+        } else if constexpr (LN) {  // rstd * (acc - mean * wsum); the pass adds ln_bias
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            st[(16 * i + 4 * fg + r) * WN_PAD + 16 * j + fr] =
+                __builtin_fmaf(lra[r], acc[h * (FM / NPASS) + i][j][r], lrc[r] * lnws[j]);
         } else {
 #pragma unroll
           for (int r = 0; r < 4; ++r) st[(16 * i + 4 * fg + r) * WN_PAD + 16 * j + fr] = acc[h * (FM / NPASS) + i][j][r];
         }
       }
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -676,7 +768,7 @@ int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
     while (ksplit > 1 && (long)ksplit * p.M * p.N > ws_floats) --ksplit;
   }
   p.ksplit = ksplit > 1 ? ksplit : 1;
-  constexpr int NT = 64 * WMW * WNW;
+  constexpr int NTH = 64 * WMW * WNW;
   p.kchunk = (nk + p.ksplit - 1) / p.ksplit;
   p.part = p.ksplit > 1 ? ws : nullptr;
   p.prio = g_prio;
@@ -688,13 +780,14 @@ int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
     // tiles: 3-stage where it fits in LDS -- measured crossovers on MI355X.
     const int stages = g_stages ? g_stages : ((WMW * WNW == 4 && ntiles * p.ksplit >= 300) ? 2 : 3);
     constexpr bool FITS3 = 3 * ((BM + BN) * 64 * 2 + 1024 + keep_stage_bytes<BM, BN, MODE>()) +
-                               (keep_stage_bytes<BM, BN, MODE>() ? KEEP_LUT_BYTES : 0) <= 160 * 1024;
+                               (keep_stage_bytes<BM, BN, MODE>() ? KEEP_LUT_BYTES : 0) +
+                               ((MODE == MODE_GEMM_LN || MODE == MODE_GEGLU_LN) ? BM * 8 + BN * 8 : 0) <= 160 * 1024;
     if constexpr (FITS3) {
-      if (stages == 2) gemm_kernel<BM, BN, WMW, WNW, MODE, 2, 64><<<grid, NT, 0, s>>>(p);
-      else gemm_kernel<BM, BN, WMW, WNW, MODE, 3, 64><<<grid, NT, 0, s>>>(p);
+      if (stages == 2) gemm_kernel<BM, BN, WMW, WNW, MODE, 2, 64><<<grid, NTH, 0, s>>>(p);
+      else gemm_kernel<BM, BN, WMW, WNW, MODE, 3, 64><<<grid, NTH, 0, s>>>(p);
     } else {
       (void)stages;
-      gemm_kernel<BM, BN, WMW, WNW, MODE, 2, 64><<<grid, NT, 0, s>>>(p);
+      gemm_kernel<BM, BN, WMW, WNW, MODE, 2, 64><<<grid, NTH, 0, s>>>(p);
     }
   }
   SDMOE_CHECK_LAUNCH();
@@ -709,20 +802,21 @@ int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
 }
 
 // routed-GEGLU linear: BN in {160, 320} tiles only (wave tile width 80 = 40 neurons = whole experts), no split-K
+template <int MODE>
 int dispatch_geglu(const GemmParams& p, hipStream_t s) {
   const int nt320 = ((p.M + 255) / 256) * (p.N / 320);
   const int nt160_128 = ((p.M + 127) / 128) * (p.N / 160);
-  if (g_tile == 1) return launch_tile<128, 160, 2, 2, MODE_GEGLU>(p, nullptr, 0, s);
-  if (g_tile == 4) return launch_tile<256, 160, 4, 2, MODE_GEGLU>(p, nullptr, 0, s);
+  if (g_tile == 1) return launch_tile<128, 160, 2, 2, MODE>(p, nullptr, 0, s);
+  if (g_tile == 4) return launch_tile<256, 160, 4, 2, MODE>(p, nullptr, 0, s);
   if (p.N % 320 == 0 && nt320 >= 240) {
     // 2x4 waves (wave tile 128 rows x 40 neurons): with the row-fastest epilogue its 32-row staging passes are
     // conflict-free (4x2's 16-row passes are not: two 16-lane b128 groups mix column pairs); 174.6 vs 181.2 us at
     // M = 65536, 129.8 vs 132.9 at 16384, 103.4 vs 106.4 at 4096 (same box)
-    if (g_tile == 5) return launch_tile<256, 320, 4, 2, MODE_GEGLU>(p, nullptr, 0, s);
-    return launch_tile<256, 320, 2, 4, MODE_GEGLU>(p, nullptr, 0, s);
+    if (g_tile == 5) return launch_tile<256, 320, 4, 2, MODE>(p, nullptr, 0, s);
+    return launch_tile<256, 320, 2, 4, MODE>(p, nullptr, 0, s);
   }
-  if (nt160_128 >= 200 || p.M > 2048) return launch_tile<128, 160, 2, 2, MODE_GEGLU>(p, nullptr, 0, s);
-  return launch_tile<64, 160, 2, 2, MODE_GEGLU>(p, nullptr, 0, s);
+  if (nt160_128 >= 200 || p.M > 2048) return launch_tile<128, 160, 2, 2, MODE>(p, nullptr, 0, s);
+  return launch_tile<64, 160, 2, 2, MODE>(p, nullptr, 0, s);
 }
 
 template <int MODE>
@@ -845,6 +939,36 @@ __global__ __launch_bounds__(256) void wmask_kmajor_kernel(const uint8_t* __rest
   }
 }
 
+// LayerNorm fold (sdmoe_ln_fold): one block per output row n of W [N, K]:
+//   Wf[n, k] = fp16(W[n, k] * gamma[k]); wsum[n] = sum_k Wf[n, k]; bias_f[n] = bias[n] + sum_k W[n, k] * beta[k]
+// (fp32; fixed-order block reduction, so the fold is deterministic)
+__global__ __launch_bounds__(256) void ln_fold_kernel(const half_t* __restrict__ W, long ldw, int K,
+                                                      const half_t* __restrict__ gamma, const half_t* __restrict__ beta,
+                                                      const half_t* __restrict__ bias, half_t* __restrict__ Wf, long ldf,
+                                                      float* __restrict__ bias_f, float* __restrict__ wsum) {
+  __shared__ float red[2][256];
+  const int n = blockIdx.x, tid = threadIdx.x;
+  float sw = 0.f, sb = 0.f;
+  for (int k = tid; k < K; k += 256) {
+    const float w = (float)W[(long)n * ldw + k];
+    const half_t wf = (half_t)(w * (float)gamma[k]);
+    Wf[(long)n * ldf + k] = wf;
+    sw += (float)wf;
+    sb = __builtin_fmaf(w, (float)beta[k], sb);
+  }
+  red[0][tid] = sw;
+  red[1][tid] = sb;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) { red[0][tid] += red[0][tid + o]; red[1][tid] += red[1][tid + o]; }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    wsum[n] = red[0][0];
+    bias_f[n] = red[1][0] + (bias ? (float)bias[n] : 0.f);
+  }
+}
+
 int grid_for(long n) {
   long g = (n + 255) / 256;
   return (int)(g > 4096 ? 4096 : (g < 1 ? 1 : g));
@@ -919,7 +1043,54 @@ extern "C" int sdmoe_linear_geglu(const void* A, long lda, const void* W, long l
   const long ab = ((long)(M - 1) * lda + K) * 2, wb = ((long)(2 * F - 1) * ldw + K) * 2;
   if (ab >= (long)OOB || wb >= (long)OOB) return SDMOE_ESHAPE;
   p.a_bytes = (int)ab; p.w_bytes = (int)wb;
-  return dispatch_geglu(p, (hipStream_t)stream);
+  return dispatch_geglu<MODE_GEGLU>(p, (hipStream_t)stream);
+}
+
+extern "C" int sdmoe_ln_fold(const void* W, long ldw, int N, int K, const void* gamma, const void* beta,
+                             const void* bias, void* Wf, long ldf, float* bias_f, float* wsum, void* stream) {
+  if (N == 0) return SDMOE_OK;
+  if (!W || !gamma || !beta || !Wf || !bias_f || !wsum || N < 0 || K <= 0 || ldw < K || ldf < K) return SDMOE_EARG;
+  ln_fold_kernel<<<N, 256, 0, (hipStream_t)stream>>>((const half_t*)W, ldw, K, (const half_t*)gamma,
+                                                     (const half_t*)beta, (const half_t*)bias, (half_t*)Wf, ldf,
+                                                     bias_f, wsum);
+  SDMOE_CHECK_LAUNCH();
+  return SDMOE_OK;
+}
+
+extern "C" int sdmoe_linear_ln(const void* A, long lda, const void* Wf, long ldw, const float* bias_f,
+                               const float* wsum, float eps, void* C, long ldc, int M, int N, int K, void* stream) {
+  if (M == 0) return SDMOE_OK;
+  if (!A || !Wf || !bias_f || !wsum || !C || M < 0 || N <= 0 || K <= 0) return SDMOE_EARG;
+  if (K % 64 || N % 8 || lda % 8 || ldw % 8 || ldc % 8) return SDMOE_ESHAPE;
+  GemmParams p{};
+  p.A = (const half_t*)A; p.lda = lda; p.W = (const half_t*)Wf; p.ldw = ldw;
+  p.C = (half_t*)C; p.ldc = ldc;
+  p.M = M; p.N = N; p.K = K; p.act = ACT_NONE; p.rows_per_batch = 1;
+  p.ln_wsum = wsum; p.ln_bias = bias_f; p.ln_eps = eps;
+  const long ab = ((long)(M - 1) * lda + K) * 2, wb = ((long)(N - 1) * ldw + K) * 2;
+  if (ab >= (long)OOB || wb >= (long)OOB) return SDMOE_ESHAPE;
+  p.a_bytes = (int)ab; p.w_bytes = (int)wb;
+  return dispatch<MODE_GEMM_LN>(p, nullptr, 0, (hipStream_t)stream);  // no split-K: a tile's K loop sees whole rows
+}
+
+extern "C" int sdmoe_linear_geglu_ln(const void* A, long lda, const void* W, long ldw, const float* bias_f,
+                                     const float* wsum, float eps, void* P, long ldp, int M, int F, int K, int act,
+                                     void* score, long ld_score, int esize, void* stream) {
+  if (M == 0) return SDMOE_OK;
+  if (!A || !W || !bias_f || !wsum || !P || M < 0 || F <= 0 || K <= 0) return SDMOE_EARG;
+  if (K % 64 || F % 80 || lda % 8 || ldw % 8 || ldp % 8) return SDMOE_ESHAPE;
+  if (score && (esize <= 0 || 40 % esize || ld_score < F / esize)) return SDMOE_ESHAPE;
+  if (!(act == ACT_GELU || act == ACT_RELU || act == ACT_NONE || act == ACT_SILU)) return SDMOE_EUNSUP;
+  GemmParams p{};
+  p.A = (const half_t*)A; p.lda = lda; p.W = (const half_t*)W; p.ldw = ldw;
+  p.C = (half_t*)P; p.ldc = ldp;
+  p.M = M; p.N = 2 * F; p.K = K; p.act = act; p.rows_per_batch = 1;
+  p.score = (half_t*)score; p.ld_score = ld_score; p.esize = esize;
+  p.ln_wsum = wsum; p.ln_bias = bias_f; p.ln_eps = eps;
+  const long ab = ((long)(M - 1) * lda + K) * 2, wb = ((long)(2 * F - 1) * ldw + K) * 2;
+  if (ab >= (long)OOB || wb >= (long)OOB) return SDMOE_ESHAPE;
+  p.a_bytes = (int)ab; p.w_bytes = (int)wb;
+  return dispatch_geglu<MODE_GEGLU_LN>(p, (hipStream_t)stream);
 }
 
 extern "C" int sdmoe_conv3x3(const void* X, long ldx, int nimg, int H, int W, int Cin,

@@ -26,6 +26,9 @@ SIGNATURES = {
     "sdmoe_groupnorm_stats": [_P, _L, _I, _I, _I, _I, _P, _P, _F, _P, _P, _P, _L, _P],
     "sdmoe_groupnorm": [_P, _L, _I, _I, _I, _I, _P, _P, _F, _I, _P, _L, _P, _P, _P, _L, _P],
     "sdmoe_layernorm": [_P, _L, _P, _L, _I, _I, _P, _P, _F, _P],
+    "sdmoe_ln_fold": [_P, _L, _I, _I, _P, _P, _P, _P, _L, _P, _P, _P],
+    "sdmoe_linear_ln": [_P, _L, _P, _L, _P, _P, _F, _P, _L, _I, _I, _I, _P],
+    "sdmoe_linear_geglu_ln": [_P, _L, _P, _L, _P, _P, _F, _P, _L, _I, _I, _I, _I, _P, _L, _I, _P],
     "sdmoe_attention": [_P, _L, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _I, _F, _P],
     "sdmoe_geglu_route": [_P, _L, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _L, _P, _L, _P, _P, _P],
     "sdmoe_linear_geglu": [_P, _L, _P, _L, _P, _P, _L, _I, _I, _I, _I, _P, _L, _I, _P],

@@ -275,6 +275,50 @@ def layernorm(x, gamma, beta, eps=1e-5, out=None):
     return out
 
 
+class LNFold:
+    """LayerNorm(gamma, beta) folded into a following linear W [N, K] (+ bias): wf = fp16(W diag(gamma)), bias_f =
+    bias + W beta and wsum = rowsum(wf) in fp32 (sdmoe_ln_fold) — the operands of sdmoe_linear_ln /
+    sdmoe_linear_geglu_ln. Built once per (weight, norm) version by the owning module."""
+
+    def __init__(self, w, gamma, beta, eps, bias=None):
+        lib = _lib.load()
+        N, K = w.shape
+        self.eps = float(eps)
+        self.w = torch.empty((N, K), dtype=torch.float16, device=w.device)
+        self.bias = torch.empty(N, dtype=torch.float32, device=w.device)
+        self.wsum = torch.empty(N, dtype=torch.float32, device=w.device)
+        if bias is not None:
+            _dev(bias, "bias")
+        st = lib.sdmoe_ln_fold(_dev(w, "w"), w.stride(0), N, K, _dev(gamma, "gamma"), _dev(beta, "beta"), _ptr(bias),
+                               self.w.data_ptr(), K, self.bias.data_ptr(), self.wsum.data_ptr(), _stream())
+        _lib.check(st, "sdmoe_ln_fold")
+
+    def rows(self, idx):
+        """The fold with its rows reordered (torch index tensor): a view-free copy for permuted layouts."""
+        f = LNFold.__new__(LNFold)
+        f.eps, f.w, f.bias, f.wsum = self.eps, self.w[idx].contiguous(), self.bias[idx].contiguous(), \
+            self.wsum[idx].contiguous()
+        return f
+
+
+def linear_ln(x, fold: LNFold, out=None):
+    """out = LayerNorm(x) @ W^T + bias with the norm folded into the GEMM (sdmoe_linear_ln): x is the
+    un-normalised [M, K] input; no normalised copy of x is written."""
+    lib = _lib.load()
+    xp, lda = _rows(x, "x")
+    M, K = x.shape
+    N = fold.w.shape[0]
+    if fold.w.shape[1] != K:
+        raise ValueError(f"linear_ln: folded weight {tuple(fold.w.shape)} does not match input K={K}")
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float16, device=x.device)
+    op, ldc = _rows(out, "out")
+    st = lib.sdmoe_linear_ln(xp, lda, fold.w.data_ptr(), fold.w.stride(0), fold.bias.data_ptr(), fold.wsum.data_ptr(),
+                             fold.eps, op, ldc, M, N, K, _stream())
+    _lib.check(st, "sdmoe_linear_ln")
+    return out
+
+
 def attention(q, k, v, nimg, Nq, Nk, heads, out=None, scale=None):
     """softmax(q k^T * scale) v per (image, head); q [nimg*Nq, heads*d], k/v [nimg*Nk, heads*d] views."""
     lib = _lib.load()
@@ -342,10 +386,33 @@ def interleave_geglu(weight: torch.Tensor, bias: torch.Tensor | None, perm: torc
     return w_il, b_il
 
 
-def linear_geglu(x, w_il, b_il, act=ACT_GELU, *, score=None, esize=0, out=None):
+def interleave_ln_fold(fold: LNFold, perm: torch.Tensor | None) -> LNFold:
+    """An LNFold of proj.weight [2F, K] with its rows in interleave_geglu's order."""
+    F = fold.w.shape[0] // 2
+    dev = fold.w.device
+    idx = torch.arange(F, device=dev) if perm is None else perm.to(dev)
+    rows = torch.stack([idx.view(F // 8, 8), (idx + F).view(F // 8, 8)], 1).reshape(2 * F)
+    return fold.rows(rows)
+
+
+def linear_geglu(x, w_il, b_il, act=ACT_GELU, *, score=None, esize=0, out=None, ln: LNFold | None = None):
     """P = value * act(gate) from the interleaved projection (interleave_geglu), plus per-expert gate sums
-    into score [M, E] (experts = contiguous esize-neuron slices) when given."""
+    into score [M, E] (experts = contiguous esize-neuron slices) when given. ln (interleave_ln_fold): x is the
+    un-normalised input and the LayerNorm is folded into the GEMM (w_il / b_il are then ignored)."""
     lib = _lib.load()
+    if ln is not None:
+        xp, lda = _rows(x, "x")
+        M, K = x.shape
+        F = ln.w.shape[0] // 2
+        if out is None:
+            out = torch.empty((M, F), dtype=torch.float16, device=x.device)
+        op, ldp = _rows(out, "out")
+        sp, lds = (None, 0) if score is None else _rows(score, "score")
+        st = lib.sdmoe_linear_geglu_ln(xp, lda, ln.w.data_ptr(), ln.w.stride(0), ln.bias.data_ptr(),
+                                       ln.wsum.data_ptr(), ln.eps, op, ldp, M, F, K, act, sp, lds, int(esize),
+                                       _stream())
+        _lib.check(st, "sdmoe_linear_geglu_ln")
+        return out
     xp, lda = _rows(x, "x")
     M, K = x.shape
     F = w_il.shape[0] // 2

@@ -17,6 +17,8 @@ Everything else is MI355X-first:
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -27,6 +29,9 @@ from .config import UNetConfig
 CTX_LEN = 77
 FUSED_GEGLU = True  # fused projection+GEGLU(+expert scores) path where eligible (tests flip it for A/B parity)
 FUSED_KEEP = True   # fused path: top-k mask applied inside the down projection (sdmoe_linear_keep) instead of a pass
+# BasicTransformerBlock LayerNorms folded into the QKV / Q / GEGLU projection GEMMs (SDMOE_FUSED_LN=0: explicit, A/B)
+FUSED_LN = os.environ.get("SDMOE_FUSED_LN", "1") != "0"
+FUSED_LN_FFN = os.environ.get("SDMOE_FUSED_LN_FFN", "0") == "1"  # norm3 into the GEGLU GEMM too (slower, see run)
 IN_PAD = 64    # conv_in input channels padded 4 -> 64 (K-step of the implicit GEMM)
 OUT_PAD = 8    # conv_out output channels padded 4 -> 8 (16-B epilogue stores)
 
@@ -130,6 +135,12 @@ class GEGLU(nn.Module):
         self._out_keep = None  # (keep bits, output pointer) when the top-k mask is left to the down projection
         self._il_key = None
         self._il = None
+        # LayerNorm deferred into the projection GEMM (FeedForward.run, FUSED_LN): (the un-normalised input view
+        # handed to this module's call, its Norm). routed()/scored()/dense() fold it into the GEMM on the fused
+        # path and apply it explicitly on every other path, so a caller of those methods always gets LN(x) semantics
+        self._ln_pending = None
+        self._il_ln_key = None
+        self._il_ln = None
 
     @property
     def inner_dim(self):
@@ -158,6 +169,21 @@ class GEGLU(nn.Module):
             self._il_key = key
         return self._il
 
+    def _take_ln(self, x):
+        """The Norm deferred into this call when x is the pending un-normalised input, else None."""
+        pend = self._ln_pending
+        return pend[1] if pend is not None and x is pend[0] else None
+
+    def _interleaved_ln(self, routing, norm):
+        w, b = self.proj.weight, self.proj.bias
+        key = (id(routing), w.data_ptr(), w._version, None if b is None else (b.data_ptr(), b._version),
+               norm.weight.data_ptr(), norm.weight._version, norm.bias.data_ptr(), norm.bias._version)
+        if self._il_ln_key != key:
+            fold = ops.LNFold(w.data, norm.weight.data, norm.bias.data, norm.eps, None if b is None else b.data)
+            self._il_ln = ops.interleave_ln_fold(fold, routing.perm if routing is not None else None)
+            self._il_ln_key = key
+        return self._il_ln
+
     def routed(self, x, removed=None, want_gate=False, sel_out=None):
         """proj GEMM + routed GEGLU kernel. x: [..., C] fp16. Returns (out [..., 4C], masked gate or None).
         sel_out (optional int32 [tokens, ceil(E/32)]) receives the per-token top-k expert bitmask.
@@ -167,18 +193,24 @@ class GEGLU(nn.Module):
         the top-k mask; `out` is then in the expert-major neuron order (self._out_perm records it)."""
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
+        norm = self._take_ln(x)
         routing = self.routing()
         act = act_code(self.gelu)
         self._out_perm = None
         self._out_keep = None
         if (FUSED_GEGLU and self._allow_permuted_out and not want_gate and self.inner_dim % 80 == 0 and x2.shape[1] % 64 == 0
                 and (routing is None or routing.fusable)):
-            w_il, b_il = self._interleaved(routing)
+            if norm is not None:
+                w_il = b_il = None
+                lnf = self._interleaved_ln(routing, norm)
+            else:
+                w_il, b_il = self._interleaved(routing)
+                lnf = None
             if routing is None:
-                out = ops.linear_geglu(x2, w_il, b_il, act)
+                out = ops.linear_geglu(x2, w_il, b_il, act, ln=lnf)
             else:
                 score = torch.empty((x2.shape[0], routing.E), dtype=torch.float16, device=x.device)
-                out = ops.linear_geglu(x2, w_il, b_il, act, score=score, esize=routing.esize)
+                out = ops.linear_geglu(x2, w_il, b_il, act, score=score, esize=routing.esize, ln=lnf)
                 if FUSED_KEEP and routing.F % 64 == 0:
                     # the dropped experts' neurons are zeroed by the down projection as it reads them
                     # (sdmoe_linear_keep); `out` is then the unmasked product, an operand only FeedForward consumes
@@ -188,6 +220,8 @@ class GEGLU(nn.Module):
                     ops.moe_topk_mask(out, score, routing, removed=removed, sel_out=sel_out)
                 self._out_perm = (routing, out.data_ptr())
             return out.view(*shp[:-1], self.inner_dim), None
+        if norm is not None:
+            x2 = ops.layernorm(x2, norm.weight, norm.bias, norm.eps)
         y = self.proj.run(x2)
         gate = torch.empty((x2.shape[0], self.inner_dim), dtype=torch.float16, device=x.device) if want_gate else None
         out = ops.geglu_route(y, self.routing(), act_code(self.gelu), removed=removed, gate_out=gate, sel_out=sel_out)
@@ -200,6 +234,9 @@ class GEGLU(nn.Module):
         expert-major, recorded in _out_perm for the down projection)."""
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
+        norm = self._take_ln(x)
+        if norm is not None:
+            x2 = ops.layernorm(x2, norm.weight, norm.bias, norm.eps)
         routing = self.routing()
         act = act_code(self.gelu)
         self._out_perm = None
@@ -218,6 +255,9 @@ class GEGLU(nn.Module):
         neuron_receivers/wanda_receiver.py:37-57)."""
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
+        norm = self._take_ln(x)
+        if norm is not None:
+            x2 = ops.layernorm(x2, norm.weight, norm.bias, norm.eps)
         act = act_code(self.gelu)
         self._out_perm = None
         if FUSED_GEGLU and self.inner_dim % 80 == 0 and x2.shape[1] % 64 == 0:
@@ -259,7 +299,7 @@ class FeedForward(nn.Module):
             self._wperm_key = key
         return self._wperm
 
-    def run(self, x2d, nimg, residual):
+    def run(self, x2d, nimg, residual, ln=None):
         """GEGLU -> down projection (+ the block's residual). The fused routed GEGLU (GEGLU.routed) hands over an
         expert-permuted product whose top-k mask is still pending (applied by the down projection as it reads it);
         that intermediate must stay private to this FeedForward, so the fused path runs only when
@@ -270,12 +310,21 @@ class FeedForward(nn.Module):
         geglu, down = self.net[0], self.net[2]
         dhooks = bool(down._forward_hooks)
         masker = _sole_receiver(down, "fused_linear") if dhooks else None
-        geglu._allow_permuted_out = (not dhooks or masker is not None) and (
-            not geglu._forward_hooks or _sole_receiver(geglu, "hook_fn") is not None)
+        owner = _sole_receiver(geglu, "hook_fn") if geglu._forward_hooks else None
+        geglu._allow_permuted_out = (not dhooks or masker is not None) and (not geglu._forward_hooks or owner is not None)
+        # ln (the block's norm3): deferred into the GEGLU projection when nothing but GEGLU's own methods can see
+        # the module input (no hook, or one sdmoe receiver whose hook hands input[0] to routed()); else applied here
+        if ln is not None and geglu._forward_hooks and (
+                owner is None or getattr(type(owner), "hook_fn", None) is not getattr(owner, "_sdmoe_ln_safe_hook", 0)):
+            x2d = ops.layernorm(x2d, ln.weight, ln.bias, ln.eps)
+            ln = None
+        xv = x2d.view(nimg, -1, x2d.shape[1])
+        geglu._ln_pending = (xv, ln) if ln is not None else None
         try:
-            h = geglu(x2d.view(nimg, -1, x2d.shape[1]))
+            h = geglu(xv)
         finally:
             geglu._allow_permuted_out = False
+            geglu._ln_pending = None
         h2 = h.reshape(-1, h.shape[-1])
         perm = geglu._out_perm
         permuted = perm is not None and perm[1] == h2.data_ptr()
@@ -313,6 +362,18 @@ class Attention(nn.Module):
         self.to_out = nn.ModuleList([LoRACompatibleLinear(wo, bo), nn.Dropout(0.0)])
         self._kv_key = None
         self._kv = None
+        self._ln_key = None
+        self._ln_fold = None
+
+    def _fold(self, norm):
+        """LNFold of the query (cross) or fused QKV (self) projection with the block's norm in front."""
+        w = self.w_qkv if self.self_attn else self.to_q.weight
+        key = (w.data_ptr(), w._version, norm.weight.data_ptr(), norm.weight._version, norm.bias.data_ptr(),
+               norm.bias._version)
+        if self._ln_key != key:
+            self._ln_fold = ops.LNFold(w.data, norm.weight.data, norm.bias.data, norm.eps)
+            self._ln_key = key
+        return self._ln_fold
 
     def cross_kv(self, ctx2d):
         """K|V projection of the text context. The context is the same tensor for every denoising step of one
@@ -326,13 +387,14 @@ class Attention(nn.Module):
             self._kv_key = key
         return self._kv
 
-    def run(self, x2d, nimg, N, residual, ctx2d=None):
+    def run(self, x2d, nimg, N, residual, ctx2d=None, ln=None):
+        """ln (the block's norm1/norm2): x2d is un-normalised and the LayerNorm is folded into the projection."""
         C = x2d.shape[1]
         if self.self_attn:
-            qkv = ops.linear(x2d, self.w_qkv)
+            qkv = ops.linear(x2d, self.w_qkv) if ln is None else ops.linear_ln(x2d, self._fold(ln))
             a = ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], nimg, N, N, self.heads)
         else:
-            q = ops.linear(x2d, self.to_q.weight)
+            q = ops.linear(x2d, self.to_q.weight) if ln is None else ops.linear_ln(x2d, self._fold(ln))
             kv = self.cross_kv(ctx2d)
             a = ops.attention(q, kv[:, :C], kv[:, C:], nimg, N, ctx2d.shape[0] // nimg, self.heads)
         return self.to_out[0].run(a, residual=residual)
@@ -344,6 +406,17 @@ class BasicTransformerBlock(nn.Module):
         self.norm1, self.attn1, self.norm2, self.attn2, self.norm3, self.ff = norm1, attn1, norm2, attn2, norm3, ff
 
     def run(self, hs, nimg, N, ctx2d):
+        if FUSED_LN and hs.shape[1] % 64 == 0:
+            # norm1 / norm2 folded into the QKV / Q projections (sdmoe_linear_ln). norm3 stays explicit unless
+            # FUSED_LN_FFN: folding it into the routed-GEGLU GEMM (sdmoe_linear_geglu_ln) measured slower than
+            # sdmoe_layernorm + the fused GEGLU (193 vs 172 + 15 us at 64x64, 144 vs 127 + 9 at 32x32): the LDS row
+            # statistics cost the GEGLU main loop more than the LayerNorm pass they replace
+            hs = self.attn1.run(hs, nimg, N, residual=hs, ln=self.norm1)
+            hs = self.attn2.run(hs, nimg, N, residual=hs, ctx2d=ctx2d, ln=self.norm2)
+            if FUSED_LN_FFN:
+                return self.ff.run(hs, nimg, residual=hs, ln=self.norm3)
+            n = ops.layernorm(hs, self.norm3.weight, self.norm3.bias, self.norm3.eps)
+            return self.ff.run(n, nimg, residual=hs)
         n = ops.layernorm(hs, self.norm1.weight, self.norm1.bias, self.norm1.eps)
         hs = self.attn1.run(n, nimg, N, residual=hs)
         n = ops.layernorm(hs, self.norm2.weight, self.norm2.bias, self.norm2.eps)

@@ -91,6 +91,26 @@ int sdmoe_layernorm(const void* X, long ldx, void* Y, long ldy, int M, int C, co
                     float eps, void* stream);
 
 /*
+ * LayerNorm folded into the GEMM that consumes it (BasicTransformerBlock norm1 -> attn1 QKV, norm2 -> attn2 Q,
+ * norm3 -> ff.net.0 GEGLU projection): no normalised activation is written or re-read.
+ *  sdmoe_ln_fold (once per weight set): Wf[n, k] = fp16(W[n, k] * gamma[k]) (row stride ldf), wsum[n] = sum_k
+ *    Wf[n, k] and bias_f[n] = bias[n] + sum_k W[n, k] * beta[k] (fp32; bias may be NULL).
+ *  sdmoe_linear_ln: C[m, n] = rstd_m * (sum_k A[m, k] Wf[n, k] - mean_m * wsum[n]) + bias_f[n]
+ *    = LayerNorm(A)[m] . W[n] + bias[n], mean_m / rstd_m = 1 / sqrt(var_m + eps) over the K channels of row m,
+ *    accumulated (v_dot2_f32_f16 sums of x and x^2) from the A tiles the GEMM already stages in LDS.
+ *  sdmoe_linear_geglu_ln: sdmoe_linear_geglu with the same fold (W / bias_f / wsum interleaved like W and bias).
+ * K % 64 == 0 and K = the normalised dimension. Replaces sdmoe_layernorm + sdmoe_linear / sdmoe_linear_geglu
+ * (diffusers BasicTransformerBlock.norm1/2/3 + to_q/k/v / GEGLU.proj).
+ */
+int sdmoe_ln_fold(const void* W, long ldw, int N, int K, const void* gamma, const void* beta, const void* bias,
+                  void* Wf, long ldf, float* bias_f, float* wsum, void* stream);
+int sdmoe_linear_ln(const void* A, long lda, const void* Wf, long ldw, const float* bias_f, const float* wsum,
+                    float eps, void* C, long ldc, int M, int N, int K, void* stream);
+int sdmoe_linear_geglu_ln(const void* A, long lda, const void* W, long ldw, const float* bias_f, const float* wsum,
+                          float eps, void* P, long ldp, int M, int F, int K, int act, void* score, long ld_score,
+                          int esize, void* stream);
+
+/*
  * Scaled-dot-product attention, fp16: O[b, q, h*d:(h+1)*d] = softmax(Q K^T * scale) V per (image b, head h),
  * with Q [nimg*Nq, *] (stride ldq), K/V [nimg*Nk, *] (strides ldk/ldv), head h at column offset h*head_dim.
  * head_dim in {32, 40, 64, 80, 160}.

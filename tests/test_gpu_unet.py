@@ -132,6 +132,7 @@ def recording(cls):
                 self.gates.append(gate.cpu())
             self.sels.append(sel_bits_to_bool(sel, E))
             return out
+        _sdmoe_ln_safe_hook = hook_fn  # only hands input[0] to routed(): the folded norm3 path stays on
     return Rec
 
 

@@ -77,6 +77,17 @@ def main():
         r = torch.randn(M, N, device=dev).half()
         ms = timeit(lambda: ops.linear(x, w, residual=r), a.iters)
         rows.append((f"linear+res M={M} N={N} K={K}", ms, 2.0 * M * N * K / ms / 1e9))
+    # LayerNorm folded into the consuming GEMM (QKV / cross-attention Q at the three levels) vs LN + GEMM
+    for M, N, K in [(n * 4096, 960, 320), (n * 4096, 320, 320), (n * 1024, 1920, 640), (n * 1024, 640, 640),
+                    (n * 256, 3840, 1280), (n * 256, 1280, 1280)]:
+        x = torch.randn(M, K, device=dev).half()
+        w = (torch.randn(N, K, device=dev) * K ** -0.5).half()
+        gm, bt = torch.randn(K, device=dev).half(), torch.randn(K, device=dev).half()
+        fold = ops.LNFold(w, gm, bt, 1e-5)
+        ms = timeit(lambda: ops.linear_ln(x, fold), a.iters)
+        rows.append((f"linear_ln M={M} N={N} K={K}", ms, 2.0 * M * N * K / ms / 1e9))
+        ms = timeit(lambda: ops.linear(ops.layernorm(x, gm, bt, 1e-5), w), a.iters)
+        rows.append((f"  ln+linear M={M} N={N} K={K}", ms, 2.0 * M * N * K / ms / 1e9))
     # fused routed GEGLU: projection GEMM with value*act(gate) + expert-score epilogue, then the top-k mask
     for M, C in [(n * 4096, 320), (n * 1024, 640), (n * 256, 1280)]:
         F, E = 4 * C, C // 5
@@ -90,6 +101,11 @@ def main():
         ms = timeit(lambda: ops.linear_geglu(x, w_il, b_il, ops.ACT_RELU, score=score, esize=routing.esize, out=out),
                     a.iters)
         rows.append((f"geglu-gemm M={M} F={F} K={C}", ms, 2.0 * M * 2 * F * C / ms / 1e9))
+        gm, bt = torch.randn(C, device=dev).half(), torch.randn(C, device=dev).half()
+        lnf = ops.interleave_ln_fold(ops.LNFold(w, gm, bt, 1e-5, b), routing.perm)
+        ms = timeit(lambda: ops.linear_geglu(x, None, None, ops.ACT_RELU, score=score, esize=routing.esize, out=out,
+                                             ln=lnf), a.iters)
+        rows.append((f"geglu-gemm-ln M={M} F={F} K={C}", ms, 2.0 * M * 2 * F * C / ms / 1e9))
         score.copy_(torch.randn(M, E, device=dev).half())
         ms = timeit(lambda: ops.moe_topk_mask(out, score, routing), a.iters)
         rows.append((f"topk-mask M={M} F={F} (GB/s)", ms, (M * F * 2 * 0.8 + M * E * 2) / ms / 1e6))

@@ -30,16 +30,28 @@ def key_flops(name, a, k, out):
         M, K = x.shape
         N = w.shape[0]
         return (f"linear M={M} N={N} K={K}", 2.0 * M * N * K, 0)
+    if name == "linear_ln":
+        x, f = a[0], a[1]
+        M, K = x.shape
+        N = f.w.shape[0]
+        return (f"linear_ln M={M} N={N} K={K}", 2.0 * M * N * K, 0)
     if name == "linear_geglu":
         x, w = a[0], a[1]
         M, K = x.shape
-        N = w.shape[0]
-        return (f"geglu M={M} N={N} K={K}", 2.0 * M * N * K, 0)
+        N = (w if w is not None else k["ln"].w).shape[0]
+        return (f"geglu{'-ln' if k.get('ln') is not None else ''} M={M} N={N} K={K}", 2.0 * M * N * K, 0)
     if name == "attention":
         q = a[0]
         nimg, Nq, Nk, heads = a[3], a[4], a[5], a[6]
         d = q.shape[1] // heads
         return (f"attn Nq={Nq} Nk={Nk} d={d} n={nimg}", 4.0 * nimg * heads * Nq * Nk * d, 0)
+    if name == "linear_keep":
+        x, w = a[0], a[2]
+        M, K = x.shape
+        return (f"linear_keep M={M} N={w.shape[0]} K={K}", 2.0 * M * w.shape[0] * K, 0)
+    if name == "groupnorm":
+        x = a[0]
+        return (f"groupnorm {tuple(x.shape)}", 0, x.numel() * 2 * 3)
     if name in ("groupnorm_stats", "groupnorm_apply", "layernorm"):
         x = a[0]
         return (f"{name} {tuple(x.shape)}", 0, x.numel() * 2 * (1 if name == "groupnorm_stats" else 2))
@@ -76,7 +88,7 @@ def main():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--evals", type=int, default=2)
     a = ap.parse_args()
-    for n in ("conv3x3_launch", "linear", "linear_geglu", "attention", "groupnorm_stats", "groupnorm_apply",
+    for n in ("conv3x3_launch", "linear", "linear_ln", "linear_geglu", "linear_keep", "groupnorm", "attention", "groupnorm_stats", "groupnorm_apply",
               "layernorm", "moe_topk_mask", "add", "mask_weight", "geglu_route"):
         wrap(n)
     from sdmoe.config import UNetConfig
