@@ -16,6 +16,8 @@
 // deterministic ordered reduce kernel that also runs the epilogue.
 // Epilogue (fused): + bias[n] + coladd[image][n] (time embedding) -> activation -> + residual[m][n],
 // staged through LDS so stores are 16 B per lane.
+#include <type_traits>
+
 #include "common.h"
 #include "../../include/sdmoe.h"
 
@@ -135,104 +137,30 @@ template <int BM, int BN, int MODE>
 constexpr int keep_stage_bytes() { return keep_a_bytes<BM, MODE>() + keep_w_bytes<BN, MODE>(); }
 constexpr int KEEP_LUT_BYTES = 16 * 8;  // 4 keep bits -> 4 x 16-bit lane masks
 
-// Routed-GEGLU epilogue over one staged pass (rows x WN fp32 in LDS, row stride WN_PAD) of a wave's tile
-// whose columns n0..n0+WN-1 are [value 8 | gate 8] chunk pairs. Rounds exactly like the unfused path
-// (fp16 linear output, fp16 act, fp16 product; expert score = fp32 sum in neuron order, rounded to fp16).
-// LDS access is row-fastest (lane -> row id % ROWS): the 16 lanes of a b128 access phase then read 16 rows of one
-// column, which the odd 16-B row stride (WN_PAD = WN + 4) spreads over all 64 banks. (Column-fastest, 16 floats apart
-// per lane, was 3-way conflicted: 1.9e7 conflict cycles per launch at 64x64.)
-template <int S, int WN, int WN_PAD, int ROWS>
-SDMOE_DEV void expert_sums(const GemmParams& p, const float* st, int mrow0, int n0, int lane) {
-  constexpr int NE = (WN / 2) / S;
-  for (int id = lane; id < ROWS * NE; id += 64) {
-    const int r = id % ROWS, e = id / ROWS;
+// Routed-GEGLU expert scores over one staged pass of a wave's tile: the activated gates (fp16) of RG rows x NH
+// neurons, experts = contiguous S-neuron slices (neurons pre-permuted expert-major). score = fp32 sum in neuron order,
+// rounded to fp16 (as sdmoe_geglu_route). Row-fastest lane mapping (lane -> row id % RG).
+template <int S, int NH, int RG>
+SDMOE_DEV void expert_sums(const GemmParams& p, const half_t* sg, int mrow0, int n0, int lane) {
+  constexpr int NE = NH / S;
+  for (int id = lane; id < RG * NE; id += 64) {
+    const int r = id % RG, e = id / RG;
     const int m = mrow0 + r;
-    const float* rp = st + r * WN_PAD + 8;
-    float v[S];
-    if constexpr (S % 4 == 0) {  // whole aligned quads of one gate chunk: b128 reads
+    const half_t* rp = sg + r * NH + e * S;
+    float acc = 0.f;
+    if constexpr (S % 4 == 0) {  // 8-B aligned quads
 #pragma unroll
       for (int q = 0; q < S / 4; ++q) {
-        const int nn = e * S + 4 * q;
-        const float4v x = *reinterpret_cast<const float4v*>(rp + 16 * (nn >> 3) + (nn & 7));
+        const half4 x = *reinterpret_cast<const half4*>(rp + 4 * q);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[4 * q + i] = x[i];
+        for (int t = 0; t < 4; ++t) acc += (float)x[t];
       }
     } else {
 #pragma unroll
-      for (int t = 0; t < S; ++t) v[t] = rp[16 * ((e * S + t) >> 3) + ((e * S + t) & 7)];
+      for (int t = 0; t < S; ++t) acc += (float)rp[t];
     }
-    float acc = 0.f;
-#pragma unroll
-    for (int t = 0; t < S; ++t) acc += v[t];  // neuron order, as the unfused kernel
     if (p.diag & 8) asm volatile("" ::"v"(acc));
     else if (m < p.M) p.score[(long)m * p.ld_score + n0 / 2 / S + e] = (half_t)acc;
-  }
-}
-
-// bias of this lane's chunk pairs (the same in every pass): up to GB iterations of the id loop below
-template <int WN, int WN_PAD, int ROWS>
-SDMOE_DEV void geglu_pass(const GemmParams& p, float* st, int mrow0, int n0, int lane, const float* gbias) {
-  constexpr int PPR = WN / 16;  // chunk pairs per row
-  constexpr int rows = ROWS;
-  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-#pragma unroll
-  for (int it = 0; it < (ROWS * PPR + 63) / 64; ++it) {
-    const int id = lane + 64 * it;
-    if (id >= rows * PPR) break;
-    const int r = id % rows, j = id / rows;  // row-fastest: conflict-free b128 LDS phases (see expert_sums)
-    const int m = mrow0 + r, n = n0 + 16 * j;
-    float* sp = st + r * WN_PAD + 16 * j;
-    const float* bp = gbias + 16 * j;
-    float x[16], bb[16];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float4v a = *reinterpret_cast<const float4v*>(sp + 4 * q), c = *reinterpret_cast<const float4v*>(bp + 4 * q);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) { x[4 * q + i] = a[i]; bb[4 * q + i] = c[i]; }
-    }
-    // fp16 linear outputs (fp32 acc + bias, rounded once), then act / product on packed halves: the product of
-    // two fp16 values is exact in fp32, so the packed fp16 multiply rounds identically
-    h2 yh[4], yg[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      yh[t] = (h2){(half_t)(x[2 * t] + bb[2 * t]), (half_t)(x[2 * t + 1] + bb[2 * t + 1])};
-      yg[t] = (h2){(half_t)(x[8 + 2 * t] + bb[8 + 2 * t]), (half_t)(x[9 + 2 * t] + bb[9 + 2 * t])};
-    }
-    h2 ga[4];
-    if (p.act == ACT_RELU) {
-#pragma unroll
-      for (int t = 0; t < 4; ++t) ga[t] = __builtin_elementwise_max(yg[t], (h2){(half_t)0.f, (half_t)0.f});
-    } else {
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-        ga[t] = (h2){(half_t)apply_act((float)yg[t][0], p.act), (half_t)apply_act((float)yg[t][1], p.act)};
-    }
-    half8 o;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const h2 pr = yh[t] * ga[t];
-      o[2 * t] = pr[0];
-      o[2 * t + 1] = pr[1];
-    }
-    // the activated gate, for the expert sums
-    *reinterpret_cast<float4v*>(sp + 8) = (float4v){(float)ga[0][0], (float)ga[0][1], (float)ga[1][0], (float)ga[1][1]};
-    *reinterpret_cast<float4v*>(sp + 12) = (float4v){(float)ga[2][0], (float)ga[2][1], (float)ga[3][0], (float)ga[3][1]};
-    if (p.diag & 8) asm volatile("" ::"v"(o));  // diagnostics: no global store
-    else if (m < p.M) *reinterpret_cast<half8*>(p.C + (long)m * p.ldc + n / 2) = o;
-  }
-  if (!p.score) return;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  switch (p.esize) {
-    case 20: expert_sums<20, WN, WN_PAD, ROWS>(p, st, mrow0, n0, lane); break;
-    case 10: expert_sums<10, WN, WN_PAD, ROWS>(p, st, mrow0, n0, lane); break;
-    case 40: expert_sums<40, WN, WN_PAD, ROWS>(p, st, mrow0, n0, lane); break;
-    case 8: expert_sums<8, WN, WN_PAD, ROWS>(p, st, mrow0, n0, lane); break;
-    case 5: expert_sums<5, WN, WN_PAD, ROWS>(p, st, mrow0, n0, lane); break;
-    case 4: expert_sums<4, WN, WN_PAD, ROWS>(p, st, mrow0, n0, lane); break;
-    case 2: expert_sums<2, WN, WN_PAD, ROWS>(p, st, mrow0, n0, lane); break;
-    default: expert_sums<1, WN, WN_PAD, ROWS>(p, st, mrow0, n0, lane); break;
   }
 }
 
@@ -265,7 +193,7 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
   constexpr int WKEEP_OFF = KEEP_OFF + keep_a_bytes<BM, MODE>();
   constexpr int STAGE = KEEP_OFF + keep_stage_bytes<BM, BN, MODE>();
   // epilogue staging: fp16 final values (row stride RS16 halves: 16-B aligned rows, conflict-free b64 stores of the
-  // swapped fragments) in NPASS16 passes; the fp32 path (GEGLU, activation, residual) in NPASS passes
+  // swapped fragments) in NPASS16 passes; the fp32 path (activation, residual) in NPASS passes; GEGLU: its own passes
   constexpr int RS16 = WN + 8;
   constexpr int NPASS16 = (NW * WM * RS16 * 2 <= NSTAGE * STAGE) ? 1 : (NW * (WM / 2) * RS16 * 2 <= NSTAGE * STAGE) ? 2
                           : ((NW * (WM / 4) * RS16 * 2 <= NSTAGE * STAGE) ? 4 : 8);
@@ -419,10 +347,9 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
   };
 
   // SWAP: C^T fragments (the MFMA's operands swapped): acc[i][j][r] = C[row wr*WM + 16 i + fr][col wc*WN + 16 j +
-  // 4 fg + r], 4 consecutive output columns of one row per lane, so the epilogue works on half4 / float4 row pieces.
-  // The routed GEGLU keeps C fragments (rows 16 i + 4 fg + r, column 16 j + fr): its epilogue measured 6 % slower
-  // on the swapped layout.
-  constexpr bool SWAP = !GEGLU;
+  // 4 fg + r], 4 consecutive output columns of one row per lane, so the epilogue works on half4 / float4 row pieces
+  // (and the routed GEGLU pairs value / gate columns with one lane swap).
+  constexpr bool SWAP = true;
   float4v acc[FM][FN];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -677,53 +604,115 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
     }
     return;
   }
-  // fp32 path (GEGLU, activation, residual): stage the raw accumulators (one b128 per fragment), then the routed
-  // GEGLU pass or epilogue8 on 8-column row chunks
-  float* st = reinterpret_cast<float*>(smem) + wave * (WM / NPASS) * WN_PAD;
-  // GEGLU: this wave's WN bias values (fp32) copied once into LDS past the staging area (per wave, no block sync)
-  float* gbias = reinterpret_cast<float*>(smem + EPI) + wave * WN;
   if constexpr (GEGLU) {
-    static_assert(EPI + NW * WN * 4 <= SMEM1, "GEGLU bias slot must fit behind the epilogue staging");
+    // Routed GEGLU on the swapped fragments, value and gate paired in registers: lane (fr, fg) holds columns
+    // 16 j + 4 fg .. +3 of row 16 i + fr, i.e. values of 4 neurons (fg 0/1) or their gates (fg 2/3, lane + 32).
+    // Two v_permlane32_swap per fragment leave lane (fr, fg) with value and gate of neurons 8 j + nsel, +1
+    // (nsel = 0, 4, 2, 6 for fg = 0..3). The fp16 product and the activated gate (both exact fp16 values) are
+    // staged in LDS per wave ([RG rows][NH neurons] each; the 16 rows x 4 lanes of a 4-B store phase hit 64
+    // distinct banks at NH = 40), then copied out as 16-B row chunks, and every (row, expert) lane sums its
+    // expert's gates in neuron order in fp32 -- the rounding points of sdmoe_linear + sdmoe_geglu_route (bit-
+    // identical). LDS traffic per wave tile: 4 x WM x NH x 2 B, a quarter of staging fp32 accumulators and bias.
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    constexpr int NH = WN / 2;                    // neurons of this wave's tile
+    constexpr int FPP = FM % 2 == 0 ? 2 : 1;      // fragment rows per staging pass
+    constexpr int RG = 16 * FPP;                  // rows per staging pass
+    constexpr int GST = NW * 2 * RG * NH * 2;     // staging bytes of all waves
+    static_assert(NH % 8 == 0, "whole 16-B product chunks per row");
+    static_assert(GST + NW * WN * 4 <= SMEM1, "GEGLU staging and bias must fit in the kernel's LDS");
+    half_t* sp = reinterpret_cast<half_t*>(smem) + wave * 2 * RG * NH;  // products [RG][NH]
+    half_t* sg = sp + RG * NH;                                          // activated gates [RG][NH]
+    float* gbias = reinterpret_cast<float*>(smem + GST) + wave * WN;    // this wave's WN bias values (fp32)
     for (int c = lane; c < WN; c += 64) gbias[c] = LN ? p.ln_bias[nw + c] : (float)p.bias[nw + c];
-  }
-  float lnws[LN ? FN : 1];  // GEGLU LN: wsum of this lane's column in each fragment (C layout: column 16 j + fr)
-  if constexpr (LN && !SWAP) {
-#pragma unroll
-    for (int j = 0; j < FN; ++j) lnws[j] = ln_col[wc * WN + 16 * j + fr];
-  }
-#pragma unroll
-  for (int h = 0; h < NPASS; ++h) {
-#pragma unroll
-    for (int i = 0; i < FM / NPASS; ++i) {
-      float4v lra = {0, 0, 0, 0}, lrc = {0, 0, 0, 0};  // GEGLU LN: (rstd, -mean*rstd) of rows 4 fg .. 4 fg + 3
-      if constexpr (LN && !SWAP) {
-        const int rl = wr * WM + 16 * (h * (FM / NPASS) + i) + 4 * fg;
-        const float4v r01 = *reinterpret_cast<const float4v*>(ln_row + 2 * rl);
-        const float4v r23 = *reinterpret_cast<const float4v*>(ln_row + 2 * rl + 4);
-        lra = (float4v){r01[0], r01[2], r23[0], r23[2]};
-        lrc = (float4v){r01[1], r01[3], r23[1], r23[3]};
-      }
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        if constexpr (SWAP) {
-          *reinterpret_cast<float4v*>(st + (16 * i + fr) * WN_PAD + 16 * j + 4 * fg) = acc[h * (FM / NPASS) + i][j];
-        } else if constexpr (LN) {  // rstd * (acc - mean * wsum); the pass adds ln_bias
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            st[(16 * i + 4 * fg + r) * WN_PAD + 16 * j + fr] =
-                __builtin_fmaf(lra[r], acc[h * (FM / NPASS) + i][j][r], lrc[r] * lnws[j]);
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) st[(16 * i + 4 * fg + r) * WN_PAD + 16 * j + fr] = acc[h * (FM / NPASS) + i][j][r];
-        }
-      }
-    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if constexpr (GEGLU) {
-      geglu_pass<WN, WN_PAD, WM / NPASS>(p, st, mw + h * (WM / NPASS), nw, lane, gbias);
-    } else
+    const int nsel = (fg & 1) * 4 + (fg >> 1) * 2;
+    // this lane's bias pairs in every fragment (value cols 16 j + nsel, +1; gate cols +8), hoisted out of the rows
+    float2v bvv[FN], bgg[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      bvv[j] = *reinterpret_cast<const float2v*>(gbias + 16 * j + nsel);
+      bgg[j] = *reinterpret_cast<const float2v*>(gbias + 16 * j + 8 + nsel);
+    }
+    auto stage_pass = [&](int h, auto relu_tag) {
+      constexpr bool RELU = decltype(relu_tag)::value;
+#pragma unroll
+      for (int ii = 0; ii < FPP; ++ii) {
+        const int i = h * FPP + ii;
+        float la = 0.f, lc = 0.f;
+        if constexpr (LN) {
+          const int rl = wr * WM + 16 * i + fr;
+          la = ln_row[2 * rl];
+          lc = ln_row[2 * rl + 1];
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          float4v v = acc[i][j];
+          if constexpr (LN) {  // rstd * (acc - mean * wsum); ln_bias is the bias below
+            const float4v ws = *reinterpret_cast<const float4v*>(ln_col + wc * WN + 16 * j + 4 * fg);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = __builtin_fmaf(la, v[r], lc * ws[r]);
+          }
+          const auto s02 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[0]), __float_as_uint(v[2]), false, false);
+          const auto s13 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[1]), __float_as_uint(v[3]), false, false);
+          const h2 yv = {(half_t)(__uint_as_float(s02[0]) + bvv[j][0]), (half_t)(__uint_as_float(s13[0]) + bvv[j][1])};
+          const h2 yg = {(half_t)(__uint_as_float(s02[1]) + bgg[j][0]), (half_t)(__uint_as_float(s13[1]) + bgg[j][1])};
+          h2 ga;
+          if constexpr (RELU) ga = __builtin_elementwise_max(yg, (h2){(half_t)0.f, (half_t)0.f});
+          else ga = (h2){(half_t)apply_act((float)yg[0], p.act), (half_t)apply_act((float)yg[1], p.act)};
+          const int off = (16 * ii + fr) * NH + 8 * j + nsel;
+          *reinterpret_cast<h2*>(sp + off) = yv * ga;  // fp16 x fp16 is exact in fp32: rounds like the unfused path
+          *reinterpret_cast<h2*>(sg + off) = ga;
+        }
+      }
+    };
+#pragma unroll
+    for (int h = 0; h < FM / FPP; ++h) {
+      if (p.act == ACT_RELU) stage_pass(h, std::integral_constant<bool, true>());
+      else stage_pass(h, std::integral_constant<bool, false>());
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int mr0 = mw + h * RG;
+      for (int id = lane; id < RG * (NH / 8); id += 64) {
+        const int r = id / (NH / 8), c = id - r * (NH / 8);
+        const int m = mr0 + r;
+        const half8 o = *reinterpret_cast<const half8*>(sp + r * NH + 8 * c);
+        if (p.diag & 8) asm volatile("" ::"v"(o));
+        else if (m < p.M) *reinterpret_cast<half8*>(p.C + (long)m * p.ldc + nw / 2 + 8 * c) = o;
+      }
+      if (p.score) {
+        switch (p.esize) {
+          case 20: expert_sums<20, NH, RG>(p, sg, mr0, nw, lane); break;
+          case 10: expert_sums<10, NH, RG>(p, sg, mr0, nw, lane); break;
+          case 40: expert_sums<40, NH, RG>(p, sg, mr0, nw, lane); break;
+          case 8: expert_sums<8, NH, RG>(p, sg, mr0, nw, lane); break;
+          case 5: expert_sums<5, NH, RG>(p, sg, mr0, nw, lane); break;
+          case 4: expert_sums<4, NH, RG>(p, sg, mr0, nw, lane); break;
+          case 2: expert_sums<2, NH, RG>(p, sg, mr0, nw, lane); break;
+          default: expert_sums<1, NH, RG>(p, sg, mr0, nw, lane); break;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    return;
+  }
+  // fp32 path (activation, residual): stage the raw accumulators (one b128 per fragment), then epilogue8 on
+  // 8-column row chunks
+  float* st = reinterpret_cast<float*>(smem) + wave * (WM / NPASS) * WN_PAD;
+#pragma unroll
+  for (int h = 0; h < NPASS; ++h) {
+#pragma unroll
+    for (int i = 0; i < FM / NPASS; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        *reinterpret_cast<float4v*>(st + (16 * i + fr) * WN_PAD + 16 * j + 4 * fg) = acc[h * (FM / NPASS) + i][j];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     for (int id = lane; id < (WM / NPASS) * CPR; id += 64) {
       const int r = id / CPR, c8 = id - r * CPR;
       const int m = mw + h * (WM / NPASS) + r, n = nw + c8 * 8;
