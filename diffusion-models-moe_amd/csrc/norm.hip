@@ -89,9 +89,8 @@ __global__ __launch_bounds__(256) void gn_partial_kernel(const half_t* __restric
 // Small latents (HW <= 1024: the 32x32 / 16x16 / 8x8 levels): one block per (image, chunk of WC channels holding
 // whole groups) reads its chunk of every row and writes the final scale/shift itself — one launch instead of
 // partial + finalize, whose two launch latencies dominated these 0.1-1.3 MB GroupNorms (~12 us each).
-// Same shifted sums as gn_partial_kernel; thread t owns 8-channel chunk t % nq and row phase t / nq. NT = 1024
-// threads keep NT / nq rows in flight per step (a 32x32 image's 1024 rows in ~3 steps of 4 loads instead of ~10 at
-// 256 threads: these launches were latency-bound), and the row phases are combined by a log-depth tree in LDS.
+// Same shifted sums as gn_partial_kernel; thread t owns 8-channel chunk t % nq and row phase t / nq; the row phases
+// are combined by a log-depth tree in LDS. NT = 256 (1024 keeps 4x the rows in flight but measured slower).
 template <int NT>
 __global__ __launch_bounds__(NT) void gn_small_kernel(const half_t* __restrict__ X, long ldx, int HW, int C, int G,
                                                       int WC, const half_t* __restrict__ gamma,
@@ -240,7 +239,9 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const half_t* __restrict
 }  // namespace
 
 namespace {
-int g_gn_nt = 1024;  // gn_small_kernel block size (sdmoe_tune knob 7: 256 or 1024, same-box A/B)
+// gn_small_kernel block size (sdmoe_tune knob 7: 256 or 1024). 256: the 1024-thread form measured slower on every
+// small-latent shape (16x16 C = 2560: 26.1 vs 13.4 us; pipeline 9.07 vs 9.14 img/s, same box)
+int g_gn_nt = 256;
 // statistics: gn_small_kernel for HW <= 1024, else partial sums + finalize
 int groupnorm_impl(const void* X, long ldx, int nimg, int HW, int C, int groups, const void* gamma, const void* beta,
                    float eps, float* scale, float* shift, float* workspace, long workspace_floats, void* stream) {

@@ -82,6 +82,10 @@ def load(path: str | None = None):
         fn = getattr(lib, name)
         fn.argtypes = argt
         fn.restype = ctypes.c_char_p if name == "sdmoe_version" else ctypes.c_int
+    # A/B experiments without code changes: SDMOE_TUNE="knob=value,..." (sdmoe_tune, include/sdmoe.h)
+    for kv in filter(None, os.environ.get("SDMOE_TUNE", "").split(",")):
+        k, v = kv.split("=")
+        check(lib.sdmoe_tune(int(k), int(v)), f"sdmoe_tune({kv})")
     _lib = lib
     return lib
 
