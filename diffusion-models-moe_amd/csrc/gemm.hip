@@ -1139,11 +1139,9 @@ extern "C" int sdmoe_mask_weight(const void* W, const void* bits, long N, long K
 }
 
 int sdmoe_attn_set_nqf(int v);  // attention.hip
-int sdmoe_gn_set_threads(int v);  // norm.hip
 
 extern "C" int sdmoe_tune(int knob, int value) {
   if (knob == 4) return sdmoe_attn_set_nqf(value);
-  if (knob == 7) return sdmoe_gn_set_threads(value);
   if (knob == 0 && (value == 0 || value == 2 || value == 3)) { g_stages = value; return SDMOE_OK; }
   if (knob == 1 && value >= 0 && value <= 5) { g_tile = value; return SDMOE_OK; }
   if (knob == 2 && (value == 0 || value == 32 || value == 64)) { g_bk = value; return SDMOE_OK; }

@@ -89,19 +89,17 @@ __global__ __launch_bounds__(256) void gn_partial_kernel(const half_t* __restric
 // Small latents (HW <= 1024: the 32x32 / 16x16 / 8x8 levels): one block per (image, chunk of WC channels holding
 // whole groups) reads its chunk of every row and writes the final scale/shift itself — one launch instead of
 // partial + finalize, whose two launch latencies dominated these 0.1-1.3 MB GroupNorms (~12 us each).
-// Same shifted sums as gn_partial_kernel; thread t owns 8-channel chunk t % nq and row phase t / nq; the row phases
-// are combined by a log-depth tree in LDS. NT = 256 (1024 keeps 4x the rows in flight but measured slower).
-template <int NT>
-__global__ __launch_bounds__(NT) void gn_small_kernel(const half_t* __restrict__ X, long ldx, int HW, int C, int G,
-                                                      int WC, const half_t* __restrict__ gamma,
-                                                      const half_t* __restrict__ beta, float eps,
-                                                      float* __restrict__ scale, float* __restrict__ shift) {
-  __shared__ float red[NT][17];
+// Same shifted sums as gn_partial_kernel; thread t owns 8-channel chunk t % nq and row phase t / nq.
+__global__ __launch_bounds__(256) void gn_small_kernel(const half_t* __restrict__ X, long ldx, int HW, int C, int G,
+                                                       int WC, const half_t* __restrict__ gamma,
+                                                       const half_t* __restrict__ beta, float eps,
+                                                       float* __restrict__ scale, float* __restrict__ shift) {
+  __shared__ float red[256][17];
   __shared__ float csum[2][256];
   __shared__ float refs[32];
   __shared__ float stat[32][2];
   const int chunk = blockIdx.x, img = blockIdx.y, tid = threadIdx.x;
-  const int cpg = C / G, c0 = chunk * WC, nq = WC / 8, R = NT / nq, gc = WC / cpg;
+  const int cpg = C / G, c0 = chunk * WC, nq = WC / 8, R = 256 / nq, gc = WC / cpg;
   const half_t* base = X + (long)img * HW * ldx + c0;
   if (tid < gc) refs[tid] = (float)base[tid * cpg];
   __syncthreads();
@@ -128,19 +126,15 @@ __global__ __launch_bounds__(NT) void gn_small_kernel(const half_t* __restrict__
 #pragma unroll
   for (int i = 0; i < 8; ++i) { red[tid][i] = s1[i]; red[tid][8 + i] = s2[i]; }
   __syncthreads();
-  // tree over the row phases: after the step with stride st, phases [0, st) hold the sums of [0, 2 st) (fixed order)
-  int pw = 1;
-  while (pw < R) pw <<= 1;
-  for (int st = pw >> 1; st >= 1; st >>= 1) {
-    if (ph < st && ph + st < R) {
+  for (int c = tid; c < nq; c += 256) {
+    float a[16];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) red[tid][i] += red[tid + st * nq][i];
-    }
-    __syncthreads();
-  }
-  for (int c = tid; c < nq; c += NT) {
+    for (int i = 0; i < 16; ++i) a[i] = 0.f;
+    for (int p = 0; p < R; ++p)
 #pragma unroll
-    for (int i = 0; i < 8; ++i) { csum[0][c * 8 + i] = red[c][i]; csum[1][c * 8 + i] = red[c][8 + i]; }
+      for (int i = 0; i < 16; ++i) a[i] += red[p * nq + c][i];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { csum[0][c * 8 + i] = a[i]; csum[1][c * 8 + i] = a[8 + i]; }
   }
   __syncthreads();
   if (tid < gc) {
@@ -154,7 +148,7 @@ __global__ __launch_bounds__(NT) void gn_small_kernel(const half_t* __restrict__
     stat[tid][1] = (float)(1.0 / sqrt(var + (double)eps));
   }
   __syncthreads();
-  for (int c = tid; c < WC; c += NT) {
+  for (int c = tid; c < WC; c += 256) {
     const int g = c / cpg, ch = c0 + c;
     const float sc = stat[g][1] * (float)gamma[ch];
     scale[(long)img * C + ch] = sc;
@@ -239,9 +233,6 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const half_t* __restrict
 }  // namespace
 
 namespace {
-// gn_small_kernel block size (sdmoe_tune knob 7: 256 or 1024). 256: the 1024-thread form measured slower on every
-// small-latent shape (16x16 C = 2560: 26.1 vs 13.4 us; pipeline 9.07 vs 9.14 img/s, same box)
-int g_gn_nt = 256;
 // statistics: gn_small_kernel for HW <= 1024, else partial sums + finalize
 int groupnorm_impl(const void* X, long ldx, int nimg, int HW, int C, int groups, const void* gamma, const void* beta,
                    float eps, float* scale, float* shift, float* workspace, long workspace_floats, void* stream) {
@@ -257,14 +248,9 @@ int groupnorm_impl(const void* X, long ldx, int nimg, int HW, int C, int groups,
     while (wc % 8) wc += cpg;
     while (wc < 80 && C % (2 * wc) == 0 && 2 * wc <= 256) wc *= 2;
     if (wc <= 256 && wc / cpg <= 32 && C % wc == 0) {
-      if (g_gn_nt == 256)
-        gn_small_kernel<256><<<dim3(C / wc, nimg), 256, 0, st>>>((const half_t*)X, ldx, HW, C, groups, wc,
-                                                                 (const half_t*)gamma, (const half_t*)beta, eps,
-                                                                 scale, shift);
-      else
-        gn_small_kernel<1024><<<dim3(C / wc, nimg), 1024, 0, st>>>((const half_t*)X, ldx, HW, C, groups, wc,
-                                                                   (const half_t*)gamma, (const half_t*)beta, eps,
-                                                                   scale, shift);
+      gn_small_kernel<<<dim3(C / wc, nimg), 256, 0, st>>>((const half_t*)X, ldx, HW, C, groups, wc,
+                                                          (const half_t*)gamma, (const half_t*)beta, eps, scale,
+                                                          shift);
       SDMOE_CHECK_LAUNCH();
       return SDMOE_OK;
     }
@@ -330,11 +316,5 @@ extern "C" int sdmoe_layernorm(const void* X, long ldx, void* Y, long ldy, int M
     default: return SDMOE_EUNSUP;
   }
   SDMOE_CHECK_LAUNCH();
-  return SDMOE_OK;
-}
-
-int sdmoe_gn_set_threads(int v) {
-  if (v != 256 && v != 1024) return SDMOE_EARG;
-  g_gn_nt = v;
   return SDMOE_OK;
 }

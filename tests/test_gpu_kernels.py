@@ -457,18 +457,11 @@ def test_transformer_block_ln_folded_vs_explicit():
 
 @pytest.mark.parametrize("H,C", [(32, 640), (32, 1280), (16, 1280), (16, 2560), (8, 1280), (8, 2560), (32, 960),
                                  (16, 1920)])
-@pytest.mark.parametrize("nt", [256, 1024])
-def test_groupnorm_small_block_sizes(H, C, nt):
-    """gn_small_kernel at the bench's small latents (16 images) with either block size (sdmoe_tune knob 7; 256 is
-    the default): both tree reductions match torch fp32 GroupNorm."""
-    from sdmoe import _lib
+def test_groupnorm_small_bench_shapes(H, C):
+    """gn_small_kernel (single-launch statistics) at the bench's small latents, 16 images, + apply(+SiLU)."""
     nimg, HW = 16, H * H
     x = rnd(nimg * HW, C, seed=95) * 2 + 1
     gamma, beta = rnd(C, scale=0.1, seed=96) + 1, rnd(C, scale=0.1, seed=97)
-    _lib.check(_lib.load().sdmoe_tune(7, nt), "tune")
-    try:
-        y = ops.groupnorm(x, nimg, HW, gamma, beta, 1e-5, 32, True)
-    finally:
-        _lib.check(_lib.load().sdmoe_tune(7, 256), "tune")
+    y = ops.groupnorm(x, nimg, HW, gamma, beta, 1e-5, 32, True)
     ref = F.group_norm(x.float().reshape(nimg, HW, C).permute(0, 2, 1), 32, gamma.float(), beta.float(), 1e-5)
     close(y, F.silu(ref.permute(0, 2, 1).reshape(nimg * HW, C)), tol=5e-3)
