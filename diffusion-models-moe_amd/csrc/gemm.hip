@@ -817,6 +817,7 @@ int dispatch(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
   if (g_tile == 3 && p.N % 320 == 0) return launch_tile<256, 320, 2, 4, MODE>(p, ws, ws_floats, s);
   if (g_tile == 4 && p.N % 160 == 0) return launch_tile<256, 160, 4, 2, MODE>(p, ws, ws_floats, s);
   if (g_tile == 5 && p.N % 320 == 0) return launch_tile<256, 320, 4, 2, MODE>(p, ws, ws_floats, s);
+  if (g_tile == 6 && p.N % 320 == 0) return launch_tile<128, 320, 2, 4, MODE>(p, ws, ws_floats, s);
   // 8-wave 256x320 tile (wave tile 128x80: 2.5x the MFMA work per LDS byte of 64x80) whenever it alone fills
   // the chip; 256x160 8-wave + split-K for long-K problems whose 128x160 grid is under ~1.2 waves of CUs.
   // Measured on MI355X with tools/gemm_bench.py --tile.
@@ -826,6 +827,12 @@ int dispatch(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
   // the A fragments to mask per wave): 61 vs 69 us at M = 65536, N = 320, K = 1280 (tools/gemm_bench.py --tile 5).
   // (180: the 16x16-level fused QKV, M = 4096 x N = 3840 x K = 1280 -- also SDXL's 32x32 level -- 43.8 vs 49.9 us on
   // 128x160; every other U-Net shape is outside 180..240)
+  // 32x32-level projections (M = 16384): the LayerNorm-folded QKV / Q and the plain (no residual) N = 640 GEMM on
+  // 128x320 8-wave tiles (wave tile 64x80, one workgroup per CU): 58.8 vs 62.7 us (QKV, N = 1920), 19.5 vs 22.1 us
+  // (N = 640) in a same-box tools/gpu_tile_sweep.sh run; the residual / conv shapes measured neutral or slower there
+  if ((MODE == MODE_GEMM_LN && p.M >= 8192 && p.M <= 16384 && p.N % 320 == 0) ||
+      (MODE == MODE_GEMM && !p.R && p.act == ACT_NONE && p.M >= 8192 && p.M <= 16384 && p.N == 640 && p.K <= 640))
+    return launch_tile<128, 320, 2, 4, MODE>(p, ws, ws_floats, s);
   if (p.N % 320 == 0 && nt320 >= 180) {
     if constexpr (mode_akeep(MODE)) return launch_tile<256, 320, 4, 2, MODE>(p, ws, ws_floats, s);
     return launch_tile<256, 320, 2, 4, MODE>(p, ws, ws_floats, s);
@@ -1143,7 +1150,7 @@ int sdmoe_attn_set_nqf(int v);  // attention.hip
 extern "C" int sdmoe_tune(int knob, int value) {
   if (knob == 4) return sdmoe_attn_set_nqf(value);
   if (knob == 0 && (value == 0 || value == 2 || value == 3)) { g_stages = value; return SDMOE_OK; }
-  if (knob == 1 && value >= 0 && value <= 5) { g_tile = value; return SDMOE_OK; }
+  if (knob == 1 && value >= 0 && value <= 6) { g_tile = value; return SDMOE_OK; }
   if (knob == 2 && (value == 0 || value == 32 || value == 64)) { g_bk = value; return SDMOE_OK; }
   if (knob == 3 && (value == 0 || value == 1)) { g_prio = value; return SDMOE_OK; }
   if (knob == 6 && value >= 0 && value <= 15) { g_diag = value; return SDMOE_OK; }
