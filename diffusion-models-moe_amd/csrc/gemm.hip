@@ -831,7 +831,7 @@ int dispatch(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
   // 128x320 8-wave tiles (wave tile 64x80, one workgroup per CU): 58.8 vs 62.7 us (QKV, N = 1920), 19.5 vs 22.1 us
   // (N = 640) in a same-box tools/gpu_tile_sweep.sh run; the residual / conv shapes measured neutral or slower there
   if ((MODE == MODE_GEMM_LN && p.M >= 8192 && p.M <= 16384 && p.N % 320 == 0) ||
-      (MODE == MODE_GEMM && !p.R && p.act == ACT_NONE && p.M >= 8192 && p.M <= 16384 && p.N == 640 && p.K <= 640))
+      (MODE == MODE_GEMM && !p.R && p.act == ACT_NONE && p.M >= 8192 && p.M <= 16384 && p.N == 640 && p.K == 640))
     return launch_tile<128, 320, 2, 4, MODE>(p, ws, ws_floats, s);
   if (p.N % 320 == 0 && nt320 >= 180) {
     if constexpr (mode_akeep(MODE)) return launch_tile<256, 320, 4, 2, MODE>(p, ws, ws_floats, s);
