@@ -199,6 +199,8 @@ class KernelTimer:
         M = out.shape[0]
         N = 4 if getattr(w, "_sdmoe_conv_out", False) else w.shape[0]
         self.flops += 2.0 * M * N * 9 * cin_real
+        if k.get("sc") is not None:  # folded 1x1 shortcut (sdmoe_conv3x3_sc): + 2 * M * Cout * Cin2
+            self.flops += 2.0 * M * N * k["sc"][2]
 
     def result(self):
         torch.cuda.synchronize()

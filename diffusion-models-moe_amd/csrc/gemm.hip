@@ -77,6 +77,10 @@ struct GemmParams {
   const float* ln_wsum;
   const float* ln_bias;
   float ln_eps;
+  // MODE_CONV with a folded 1x1 shortcut (sdmoe_conv3x3_sc): K-steps past the 9 * Cin conv steps read A2 [M, K2]
+  // (the block input at the output pixel, row stride lda2) against the shortcut weights appended to W's rows
+  const half_t* A2; long lda2;
+  int a2_bytes;
 };
 
 SDMOE_DEV int swz(int row) { return (row >> 1) & 7; }
@@ -241,13 +245,15 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
   unsigned avoff[A_PW];  // GEMM: byte offset of (row, pre-swizzled chunk); conv: of the centre-tap pixel
   unsigned amask[A_PW];  // conv: bit t = tap t in bounds (0 = M-tail row)
   int aoh[A_PW], aow[A_PW], ab_[A_PW];  // conv-upsample rows
+  unsigned avoff2[A_PW];  // conv + shortcut: byte offset of (output pixel row, pre-swizzled chunk) in A2
   unsigned bvoff[B_PW];
 #pragma unroll
   for (int j = 0; j < A_PW; ++j) {
     const int r = RPP * (j * NW + wave) + lrow;
     const unsigned chb = (unsigned)((lch ^ swzk(r)) * 16);
     const int m = m0 + r;
-    avoff[j] = OOB; amask[j] = 0; aoh[j] = 0; aow[j] = 0; ab_[j] = 0;
+    avoff[j] = OOB; amask[j] = 0; aoh[j] = 0; aow[j] = 0; ab_[j] = 0; avoff2[j] = OOB;
+    if (MODE == MODE_CONV && p.A2 && j * NW + wave < A_INS && m < p.M) avoff2[j] = (unsigned)((long)m * p.lda2 * 2) + chb;
     if (j * NW + wave < A_INS && m < p.M) {
       if (!CONV) {
         avoff[j] = (unsigned)((long)m * p.lda * 2) + chb;
@@ -308,7 +314,12 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
   // conv K walk: (64-channel step, tap) advanced incrementally in scalar registers. Channel-step-major: the 9
   // consecutive K-steps of one 64-channel slice re-read the same activation rows (shifted by a tap), so a
   // workgroup's A working set is ~(BM + halo) x 128 B and stays in the XCD's L2 across the taps.
+  // Folded shortcut (MODE_CONV, p.A2): channel steps st_c >= csl (= Cin / 64) are single K-steps of A2.
+  const int csl = CONV ? p.Cin / BK : 0;
+  const __amdgpu_buffer_rsrc_t rsA2 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.A2, (short)0, p.A2 ? p.a2_bytes : 0, 0x00020000);
   int st_c = CONV ? ks0 / 9 : 0, st_tap = CONV ? ks0 - st_c * 9 : 0;
+  if (MODE == MODE_CONV && ks0 >= 9 * csl) { st_c = csl + (ks0 - 9 * csl); st_tap = 0; }
 
   auto issue_stage = [&](int ks, int buf) {
     char* sa = smem + buf * STAGE;
@@ -316,6 +327,11 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
     if (!CONV) {
 #pragma unroll
       for (int j = 0; j < A_PW; ++j) bld16(rsA, sa + a_dst(j), avoff[j], kb);
+    } else if (MODE == MODE_CONV && st_c >= csl) {  // folded shortcut K-step (wave-uniform)
+      const unsigned c2b = (unsigned)((st_c - csl) * BK * 2);
+      ++st_c;
+#pragma unroll
+      for (int j = 0; j < A_PW; ++j) bld16(rsA2, sa + a_dst(j), avoff2[j] == OOB ? OOB : avoff2[j] + c2b, 0);
     } else {
       const int tap = st_tap;
       const int kh = tap >= 6 ? 2 : (tap >= 3 ? 1 : 0);
@@ -1111,6 +1127,28 @@ extern "C" int sdmoe_conv3x3(const void* X, long ldx, int nimg, int H, int W, in
   if (ab >= (long)OOB || wb >= (long)OOB) return SDMOE_ESHAPE;
   p.a_bytes = (int)ab; p.w_bytes = (int)wb;
   if (upsample) return dispatch<MODE_CONV_UP>(p, workspace, workspace_floats, (hipStream_t)stream);
+  return dispatch<MODE_CONV>(p, workspace, workspace_floats, (hipStream_t)stream);
+}
+
+extern "C" int sdmoe_conv3x3_sc(const void* X, long ldx, int nimg, int H, int W, int Cin, const void* Wt,
+                                const void* bias, const void* coladd, long coladd_bstride, const void* X2, long ldx2,
+                                int Cin2, void* Y, long ldy, int Cout, int act, float* workspace,
+                                long workspace_floats, void* stream) {
+  if (nimg == 0) return SDMOE_OK;
+  if (!X || !Wt || !X2 || !Y || nimg < 0 || H <= 0 || W <= 0 || Cout <= 0 || Cin2 <= 0) return SDMOE_EARG;
+  if (Cin % 64 || Cin2 % 64 || Cout % 8 || ldx % 8 || ldx2 % 8 || ldy % 8) return SDMOE_ESHAPE;
+  GemmParams p{};
+  p.A = (const half_t*)X; p.lda = ldx; p.W = (const half_t*)Wt; p.ldw = 9L * Cin + Cin2;
+  p.bias = (const half_t*)bias; p.coladd = (const half_t*)coladd; p.coladd_bstride = coladd_bstride;
+  p.C = (half_t*)Y; p.ldc = ldy;
+  p.M = nimg * H * W; p.N = Cout; p.K = 9 * Cin + Cin2; p.act = act;
+  p.rows_per_batch = H * W;
+  p.H = H; p.Wd = W; p.Cin = Cin; p.OH = H; p.OW = W; p.stride = 1; p.upsample = 0;
+  p.A2 = (const half_t*)X2; p.lda2 = ldx2;
+  const long ab = ((long)nimg * H * W - 1) * ldx * 2 + (long)Cin * 2, wb = (long)Cout * p.ldw * 2;
+  const long a2b = ((long)nimg * H * W - 1) * ldx2 * 2 + (long)Cin2 * 2;
+  if (ab >= (long)OOB || wb >= (long)OOB || a2b >= (long)OOB) return SDMOE_ESHAPE;
+  p.a_bytes = (int)ab; p.w_bytes = (int)wb; p.a2_bytes = (int)a2b;
   return dispatch<MODE_CONV>(p, workspace, workspace_floats, (hipStream_t)stream);
 }
 

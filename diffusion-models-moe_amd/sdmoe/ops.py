@@ -192,16 +192,39 @@ def conv_weight_from_torch(w):
     return conv_weight(w.permute(0, 2, 3, 1))
 
 
+def conv_weight_with_shortcut(w, w_sc):
+    """[Cout, 9*Cin + Cin2]: the conv3x3 weight (conv_weight layout) with a 1x1 shortcut's [Cout, Cin2] columns
+    appended — the operand of conv3x3(..., shortcut=x2) (sdmoe_conv3x3_sc)."""
+    return torch.cat([w.reshape(w.shape[0], -1), w_sc.reshape(w.shape[0], -1)], 1).contiguous()
+
+
 def conv3x3(x, nimg, H, W, w, bias=None, *, stride=1, upsample=False, out=None, residual=None, act=ACT_NONE,
-            coladd=None, coladd_bstride=0, gn=None):
+            coladd=None, coladd_bstride=0, gn=None, shortcut=None):
     """3x3 conv (pad 1) on NHWC x viewed as [nimg*H*W, Cin]; w: [Cout, Cin/64, 3, 3, 64] fp16 (conv_weight).
-    gn = (scale, shift, silu): GroupNorm(+SiLU) applied to x once (one read + write of x) before the conv."""
+    gn = (scale, shift, silu): GroupNorm(+SiLU) applied to x once (one read + write of x) before the conv.
+    shortcut = x2 [nimg*H*W, Cin2]: a 1x1 projection of x2 folded in as extra K-steps (stride 1, no residual);
+    w is then conv_weight_with_shortcut(...) [Cout, 9*Cin + Cin2]."""
     lib = _lib.load()
     if gn is not None:
         x = groupnorm_apply(x, nimg, H * W, gn[0], gn[1], gn[2])
     xp, ldx = _rows(x, "x")
     Cin = x.shape[1]
     Cout = w.shape[0]
+    if shortcut is not None:
+        x2p, ldx2 = _rows(shortcut, "shortcut")
+        Cin2 = shortcut.shape[1]
+        if w.dim() != 2 or w.shape[1] != 9 * Cin + Cin2 or Cin % 64 or Cin2 % 64:
+            raise ValueError(f"conv3x3: weight {tuple(w.shape)} is not [Cout, 9*{Cin} + {Cin2}] "
+                             "(ops.conv_weight_with_shortcut)")
+        if stride != 1 or upsample or residual is not None or shortcut.shape[0] != x.shape[0]:
+            raise ValueError("conv3x3: a folded shortcut needs stride 1, no upsample, no residual, same rows")
+        if x.shape[0] != nimg * H * W:
+            raise ValueError("conv3x3: rows != nimg*H*W")
+        if out is None:
+            out = torch.empty((nimg * H * W, Cout), dtype=torch.float16, device=x.device)
+        op, ldy = _rows(out, "out")
+        return conv3x3_launch(xp, ldx, nimg, H, W, Cin, w, bias, coladd, coladd_bstride, None, 0, out, op, ldy, Cout,
+                              1, False, act, sc=(x2p, ldx2, Cin2))
     if w.dim() != 5 or tuple(w.shape[1:]) != (Cin // 64, 3, 3, 64) or Cin % 64:
         raise ValueError(f"conv3x3: weight {tuple(w.shape)} is not the [Cout, Cin/64, 3, 3, 64] layout for "
                          f"Cin={Cin} (ops.conv_weight)")
@@ -220,10 +243,16 @@ def conv3x3(x, nimg, H, W, w, bias=None, *, stride=1, upsample=False, out=None, 
 
 
 def conv3x3_launch(xp, ldx, nimg, H, W, Cin, w, bias, coladd, coladd_bstride, rp, ldr, out, op, ldy, Cout, stride,
-                   upsample, act):
-    """The sdmoe_conv3x3 launch alone (bench.py times exactly this with HIP events)."""
+                   upsample, act, sc=None):
+    """The sdmoe_conv3x3 launch alone (bench.py times exactly this with HIP events); sc = (x2 ptr, ldx2, Cin2):
+    sdmoe_conv3x3_sc with the folded 1x1 shortcut."""
     lib = _lib.load()
     ws = _workspace(out.device)
+    if sc is not None:
+        st = lib.sdmoe_conv3x3_sc(xp, ldx, nimg, H, W, Cin, _dev(w, "w"), _ptr(bias), _ptr(coladd), coladd_bstride,
+                                  sc[0], sc[1], sc[2], op, ldy, Cout, act, ws.data_ptr(), ws.numel(), _stream())
+        _lib.check(st, "sdmoe_conv3x3_sc")
+        return out
     st = lib.sdmoe_conv3x3(xp, ldx, nimg, H, W, Cin, _dev(w, "w"), _ptr(bias), _ptr(coladd), coladd_bstride, rp, ldr,
                            op, ldy, Cout, stride, int(bool(upsample)), act, ws.data_ptr(), ws.numel(), _stream())
     _lib.check(st, "sdmoe_conv3x3")

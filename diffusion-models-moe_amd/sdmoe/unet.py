@@ -32,6 +32,8 @@ FUSED_KEEP = True   # fused path: top-k mask applied inside the down projection 
 # BasicTransformerBlock LayerNorms folded into the QKV / Q / GEGLU projection GEMMs (SDMOE_FUSED_LN=0: explicit, A/B)
 FUSED_LN = os.environ.get("SDMOE_FUSED_LN", "1") != "0"
 FUSED_LN_FFN = os.environ.get("SDMOE_FUSED_LN_FFN", "0") == "1"  # norm3 into the GEGLU GEMM too (slower, see run)
+# ResnetBlock2D conv_shortcut (1x1) folded into conv2 as extra K-steps (sdmoe_conv3x3_sc; SDMOE_FUSED_SC=0: separate)
+FUSED_SC = os.environ.get("SDMOE_FUSED_SC", "1") != "0"
 IN_PAD = 64    # conv_in input channels padded 4 -> 64 (K-step of the implicit GEMM)
 OUT_PAD = 8    # conv_out output channels padded 4 -> 8 (16-B epilogue stores)
 
@@ -449,6 +451,19 @@ class ResnetBlock2D(nn.Module):
         self.norm1, self.conv1, self.time_emb_proj, self.norm2, self.conv2 = norm1, conv1, temb_proj, norm2, conv2
         self.conv_shortcut = shortcut
         self.temb_slice = None  # (offset, Cout) into the fused time-embedding projection output
+        self._sc_key = None
+        self._sc_w = None
+
+    def _conv2_with_shortcut(self):
+        """conv2's weight with conv_shortcut's columns appended and the two biases summed (fp32, rounded once)."""
+        w2, b2, ws, bs = self.conv2.weight, self.conv2.bias, self.conv_shortcut.weight, self.conv_shortcut.bias
+        key = tuple(None if t is None else (t.data_ptr(), t._version) for t in (w2, b2, ws, bs))
+        if self._sc_key != key:
+            b = sum(t.data.float() for t in (b2, bs) if t is not None)
+            self._sc_w = (ops.conv_weight_with_shortcut(w2.data, ws.data),
+                          None if isinstance(b, int) else b.half())
+            self._sc_key = key
+        return self._sc_w
 
     def run(self, x, nimg, H, W, temb_all, out):
         HW = H * W
@@ -460,6 +475,10 @@ class ResnetBlock2D(nn.Module):
         h = ops.conv3x3(xn, nimg, H, W, self.conv1.weight, self.conv1.bias,
                         coladd=temb_all[:, o:o + n], coladd_bstride=bstride)
         hn = self.norm2.normalize(h, nimg, HW, True)
+        if self.conv_shortcut is not None and FUSED_SC and x.shape[1] % 64 == 0:
+            # conv2(hn) + conv_shortcut(x) in one implicit GEMM: the shortcut is K-steps over x at the output pixel
+            w, b = self._conv2_with_shortcut()
+            return ops.conv3x3(hn, nimg, H, W, w, b, shortcut=x, out=out)
         res = x if self.conv_shortcut is None else self.conv_shortcut.run(x)
         return ops.conv3x3(hn, nimg, H, W, self.conv2.weight, self.conv2.bias, residual=res, out=out)
 

@@ -57,6 +57,18 @@ int sdmoe_conv3x3(const void* X, long ldx, int nimg, int H, int W, int Cin, cons
                   const void* coladd, long coladd_bstride, const void* R, long ldr, void* Y, long ldy, int Cout,
                   int stride, int upsample, int act, float* workspace, long workspace_floats, void* stream);
 
+/*
+ * sdmoe_conv3x3 (stride 1) with a 1x1 projection shortcut folded in as extra K-steps:
+ *   Y = conv3x3(X; Wt[:, :9 Cin]) + X2 Wt[:, 9 Cin:]^T + bias + coladd, X2 [nimg*H*W, Cin2] (row stride ldx2).
+ * Wt [Cout][9 Cin + Cin2]: the conv weights in the sdmoe_conv3x3 layout followed by the shortcut's [Cout, Cin2]
+ * columns; bias = conv2.bias + conv_shortcut.bias. Cin2 % 64 == 0.
+ * Replaces: diffusers ResnetBlock2D conv2 + conv_shortcut + the residual add (`output_tensor = input_tensor +
+ * hidden_states` with input_tensor = conv_shortcut(input_tensor); external) — no shortcut output is written or re-read.
+ */
+int sdmoe_conv3x3_sc(const void* X, long ldx, int nimg, int H, int W, int Cin, const void* Wt, const void* bias,
+                     const void* coladd, long coladd_bstride, const void* X2, long ldx2, int Cin2, void* Y, long ldy,
+                     int Cout, int act, float* workspace, long workspace_floats, void* stream);
+
 /* Y = (SiLU?)(X * scale[img, c] + shift[img, c]) on [nimg*HW, C] (the GroupNorm apply; scale/shift from
  * sdmoe_groupnorm_stats). C % 8 == 0. */
 int sdmoe_groupnorm_apply(const void* X, long ldx, int nimg, int HW, int C, const float* scale, const float* shift,

@@ -465,3 +465,25 @@ def test_groupnorm_small_bench_shapes(H, C):
     y = ops.groupnorm(x, nimg, HW, gamma, beta, 1e-5, 32, True)
     ref = F.group_norm(x.float().reshape(nimg, HW, C).permute(0, 2, 1), 32, gamma.float(), beta.float(), 1e-5)
     close(y, F.silu(ref.permute(0, 2, 1).reshape(nimg * HW, C)), tol=5e-3)
+
+
+@pytest.mark.parametrize("H,C,Cin2,nimg", [(64, 320, 960, 2), (64, 320, 640, 3), (32, 640, 1920, 4), (32, 640, 320, 3),
+                                           (16, 1280, 2560, 16), (16, 1280, 640, 5), (8, 1280, 2560, 16),
+                                           (8, 1280, 1920, 3)])
+def test_conv3x3_folded_shortcut(H, C, Cin2, nimg):
+    """sdmoe_conv3x3_sc: conv2(hn) + conv_shortcut(x) (+ bias, per-image column add) as one implicit GEMM vs torch
+    fp32 conv2d + 1x1 projection, at the U-Net's shortcut shapes (incl. the split-K 16x16 / 8x8 levels, M tails
+    and a channel-slice shortcut input)."""
+    hn = rnd(nimg * H * H, C, seed=101)
+    buf = rnd(nimg * H * H, Cin2 + 64, seed=102)
+    x = buf[:, 64:]  # row stride > Cin2, like the concatenation buffers
+    w = rnd(C, C, 3, 3, scale=(9 * C) ** -0.5, seed=103)
+    wsc = rnd(C, Cin2, scale=Cin2 ** -0.5, seed=104)
+    b = rnd(C, scale=0.1, seed=105)
+    cadd = rnd(nimg, C, scale=0.1, seed=106)
+    wcat = ops.conv_weight_with_shortcut(ops.conv_weight_from_torch(w), wsc)
+    out = ops.conv3x3(hn, nimg, H, H, wcat, b, shortcut=x, coladd=cadd, coladd_bstride=C)
+    xi = hn.float().reshape(nimg, H, H, C).permute(0, 3, 1, 2)
+    ref = F.conv2d(xi, w.float(), b.float(), padding=1).permute(0, 2, 3, 1).reshape(-1, C)
+    ref = ref + x.float() @ wsc.float().t() + cadd.float().repeat_interleave(H * H, 0)
+    close(out, ref)
