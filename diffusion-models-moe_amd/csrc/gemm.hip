@@ -37,7 +37,7 @@ int g_tile = 0;
 int g_bk = 0;
 int g_prio = 0;
 int g_diag = 0;
-int g_spread = 1;  // knob 8  // knob 6, diagnostics only (results garbage): bit 0 = no K-loop operand loads, bit 1 = no MFMAs,
+int g_spread = 2;  // knob 8: 0 = pieces after the barrier, 1 = behind each group's MFMAs, 2 = split between its MFMA rows  // knob 6, diagnostics only (results garbage): bit 0 = no K-loop operand loads, bit 1 = no MFMAs,
                  // bit 2 = no epilogue (nothing stored), bit 3 = epilogue without its global stores
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -417,6 +417,7 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
     // piece costs ~60 issue cycles among bare MFMAs and 100-185 in a phase already carrying 8 pieces + 16 LDS reads,
     // MI355X_MICROARCH constants); else all of them here, right after the barrier
     const bool spread = p.spread && SDMOE_GEMM_PIPE && !(KEEP && FN > 5);
+    const bool spread2 = spread && p.spread == 2;
     if (do_issue) {
       if (spread) stage_prep(ks0 + it + NSTAGE - 1, (it + NSTAGE - 1) % NSTAGE);
       else issue_stage(ks0 + it + NSTAGE - 1, (it + NSTAGE - 1) % NSTAGE);
@@ -483,19 +484,26 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
             n1 = read_a(kk + 1, 1);
           }
           __builtin_amdgcn_sched_barrier(0);
+          const int gi = kk * NG + g;
 #pragma unroll
           for (int j = 0; j < FN; ++j)
             acc[2 * g][j] = SWAP ? mfma16x16x32(bcur[j], a0, acc[2 * g][j]) : mfma16x16x32(a0, bcur[j], acc[2 * g][j]);
+          if (spread2 && do_issue) {  // spread 2: the group's first half of pieces between its two MFMA rows
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < PER_WAVE; ++q)
+              if (q >= gi * PPG && q < gi * PPG + (PPG + 1) / 2) issue_piece(q);
+            __builtin_amdgcn_sched_barrier(0);
+          }
 #pragma unroll
           for (int j = 0; j < FN; ++j)
             acc[2 * g + 1][j] = SWAP ? mfma16x16x32(bcur[j], a1, acc[2 * g + 1][j])
                                      : mfma16x16x32(a1, bcur[j], acc[2 * g + 1][j]);
           __builtin_amdgcn_sched_barrier(0);
           if (spread && do_issue) {
-            const int gi = kk * NG + g;
 #pragma unroll
             for (int q = 0; q < PER_WAVE; ++q)
-              if (q >= gi * PPG && q < (gi + 1) * PPG) issue_piece(q);
+              if (q >= gi * PPG + (spread2 ? (PPG + 1) / 2 : 0) && q < (gi + 1) * PPG) issue_piece(q);
           }
           __builtin_amdgcn_sched_barrier(0);
           a0 = n0;
@@ -819,7 +827,7 @@ int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
   // tiles with long K (32x32 convs 1.5-4 %); not the 64-row / 4-wave small-K tiles (up to 20 % slower there: too few
   // MFMA groups to hide the late pieces)
   constexpr bool GEGLU_T = MODE == MODE_GEGLU || MODE == MODE_GEGLU_LN;
-  p.spread = g_spread && ((BM == 256 && (p.kchunk >= 8 || GEGLU_T)) || (BM == 128 && BN == 160 && p.kchunk >= 16));
+  p.spread = ((BM == 256 && (p.kchunk >= 8 || GEGLU_T)) || (BM == 128 && BN == 160 && p.kchunk >= 16)) ? g_spread : 0;
   const dim3 grid(ntiles * p.ksplit);
   {
     // 64-deep K-steps (a 32-deep 4/5-stage ring measured slower on every shape; the kernel is generic in BK).
@@ -1234,6 +1242,6 @@ extern "C" int sdmoe_tune(int knob, int value) {
   if (knob == 2 && (value == 0 || value == 32 || value == 64)) { g_bk = value; return SDMOE_OK; }
   if (knob == 3 && (value == 0 || value == 1)) { g_prio = value; return SDMOE_OK; }
   if (knob == 6 && value >= 0 && value <= 15) { g_diag = value; return SDMOE_OK; }
-  if (knob == 8 && (value == 0 || value == 1)) { g_spread = value; return SDMOE_OK; }
+  if (knob == 8 && value >= 0 && value <= 2) { g_spread = value; return SDMOE_OK; }
   return SDMOE_EARG;
 }

@@ -318,7 +318,8 @@ int sdmoe_cfg_multistep_step(const void* eps, long lde, float* lat, int B, int H
    depth (0 auto, 32, 64); knob 3 = MFMA-cluster wave priority (0/1); knob 4 = attention kernel (0 auto by shape,
    1 = 32x32x16 MFMA kernel, 2 / 4 = 16x16x32 kernel with 32 / 64 queries per wave, 64 for head_dim <= 40
    only); knob 6 = GEMM diagnostics bits (1 no K-loop loads, 2 no MFMA, 4 no epilogue, 8 no global stores); knob 8 =
-   GEMM LDS-DMA placement: 1 = the next stage's pieces spread over the MFMA groups, 0 = all after the barrier. */
+   GEMM LDS-DMA placement: 2 = the next stage's pieces spread over the MFMA groups, split between each group's two
+   MFMA rows (default), 1 = behind each group's MFMAs, 0 = all after the barrier. */
 int sdmoe_tune(int knob, int value);
 
 /* out = a + b (fp16, n % 8 == 0). */
