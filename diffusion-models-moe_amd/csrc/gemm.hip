@@ -36,9 +36,10 @@ int g_stages = 0;
 int g_tile = 0;
 int g_bk = 0;
 int g_prio = 0;
-int g_diag = 0;
-int g_spread = 2;  // knob 8: 0 = pieces after the barrier, 1 = behind each group's MFMAs, 2 = split between its MFMA rows  // knob 6, diagnostics only (results garbage): bit 0 = no K-loop operand loads, bit 1 = no MFMAs,
+int g_diag = 0;  // knob 6, diagnostics only (results garbage): bit 0 = no K-loop operand loads, bit 1 = no MFMAs,
                  // bit 2 = no epilogue (nothing stored), bit 3 = epilogue without its global stores
+int g_spread = 2;  // knob 8: LDS-DMA placement, 0 = all pieces after the barrier, 1 = behind each MFMA group,
+                   // 2 = split between each group's two MFMA rows
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
