@@ -824,11 +824,12 @@ int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
   p.prio = g_prio;
   p.diag = g_diag;
   // spread LDS-DMA issue where it measured faster (same-box tools/gemm_bench.py, knob 8 on vs off): 256-row tiles
-  // with >= 8 K-steps per workgroup (convs 4-6 %, K >= 640 projections 2-5 %) and the routed GEGLU (7 %), 128x160
-  // tiles with long K (32x32 convs 1.5-4 %); not the 64-row / 4-wave small-K tiles (up to 20 % slower there: too few
-  // MFMA groups to hide the late pieces)
+  // with >= 8 K-steps per workgroup (convs 4-6 %, K >= 640 projections 2-5 %) and the routed GEGLU (7 %). Not the
+  // 4-wave tiles: with 2-4 MFMA groups per K-step the last pieces go out too late to land before the next K-step
+  // (64x160: up to 20 % slower in isolation; the 128x160 32x32-level convs, neutral in isolation, ran 28 % slower in
+  // the pipeline trace where their inputs come from HBM -- r02d profile)
   constexpr bool GEGLU_T = MODE == MODE_GEGLU || MODE == MODE_GEGLU_LN;
-  p.spread = ((BM == 256 && (p.kchunk >= 8 || GEGLU_T)) || (BM == 128 && BN == 160 && p.kchunk >= 16)) ? g_spread : 0;
+  p.spread = (BM == 256 && (p.kchunk >= 8 || GEGLU_T)) ? g_spread : 0;
   const dim3 grid(ntiles * p.ksplit);
   {
     // 64-deep K-steps (a 32-deep 4/5-stage ring measured slower on every shape; the kernel is generic in BK).
