@@ -38,6 +38,7 @@ int g_bk = 0;
 int g_prio = 0;
 int g_diag = 0;  // knob 6, diagnostics only (results garbage): bit 0 = no K-loop operand loads, bit 1 = no MFMAs,
                  // bit 2 = no epilogue (nothing stored), bit 3 = epilogue without its global stores
+int g_spread_np = 1;  // knob 9
 int g_spread = 2;  // knob 8: LDS-DMA placement, 0 = all pieces after the barrier, 1 = behind each MFMA group,
                    // 2 = split between each group's two MFMA rows
 
@@ -65,6 +66,7 @@ struct GemmParams {
   int esize;
   int prio;  // experiment knob: raise wave priority around the MFMA block
   int spread;  // 1: the next stage's LDS-DMA pieces are spread over the MFMA groups (sdmoe_tune knob 8)
+  int spread_np;  // the same for the unpipelined wide masked tiles (knob 9)
   int diag;  // diagnostic knob (sdmoe_tune 6): bit 0 skips the K-loop loads, bit 1 the MFMAs
   // expert keep mask of the A operand (MODE_KEEP / MODE_KEEPW): keep[(k / 64) * M * 8 + m * 8 + (k % 64) / 8] bit
   // (k % 8) = neuron k of token m survives the top-k; the A fragments are ANDed with it after their LDS read
@@ -419,8 +421,10 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
     // MI355X_MICROARCH constants); else all of them here, right after the barrier
     const bool spread = p.spread && SDMOE_GEMM_PIPE && !(KEEP && FN > 5);
     const bool spread2 = spread && p.spread == 2;
+    // the unpipelined (wide masked) path: the pieces go out once, between its two 32-deep MFMA halves
+    const bool spread_np = p.spread && p.spread_np && !(SDMOE_GEMM_PIPE && !(KEEP && FN > 5));
     if (do_issue) {
-      if (spread) stage_prep(ks0 + it + NSTAGE - 1, (it + NSTAGE - 1) % NSTAGE);
+      if (spread || spread_np) stage_prep(ks0 + it + NSTAGE - 1, (it + NSTAGE - 1) % NSTAGE);
       else issue_stage(ks0 + it + NSTAGE - 1, (it + NSTAGE - 1) % NSTAGE);
     }
 
@@ -528,6 +532,12 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
 #pragma unroll
           for (int j = 0; j < FN; ++j)
             acc[i][j] = SWAP ? mfma16x16x32(bf[j], af[i], acc[i][j]) : mfma16x16x32(af[i], bf[j], acc[i][j]);
+        if (kk == 0 && spread_np && do_issue) {
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int q = 0; q < PER_WAVE; ++q) issue_piece(q);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
     }
     if constexpr (LN) {
@@ -830,6 +840,7 @@ int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
   // the pipeline trace where their inputs come from HBM -- r02d profile)
   constexpr bool GEGLU_T = MODE == MODE_GEGLU || MODE == MODE_GEGLU_LN;
   p.spread = (BM == 256 && (p.kchunk >= 8 || GEGLU_T)) ? g_spread : 0;
+  p.spread_np = g_spread_np;
   const dim3 grid(ntiles * p.ksplit);
   {
     // 64-deep K-steps (a 32-deep 4/5-stage ring measured slower on every shape; the kernel is generic in BK).
@@ -1245,5 +1256,6 @@ extern "C" int sdmoe_tune(int knob, int value) {
   if (knob == 3 && (value == 0 || value == 1)) { g_prio = value; return SDMOE_OK; }
   if (knob == 6 && value >= 0 && value <= 15) { g_diag = value; return SDMOE_OK; }
   if (knob == 8 && value >= 0 && value <= 2) { g_spread = value; return SDMOE_OK; }
+  if (knob == 9 && (value == 0 || value == 1)) { g_spread_np = value; return SDMOE_OK; }
   return SDMOE_EARG;
 }
