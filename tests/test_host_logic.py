@@ -433,3 +433,46 @@ def test_initial_latents_unseeded_process_seed():
     assert a.shape == (1, 4, 8, 8) and torch.isfinite(a).all()
     g = torch.Generator().manual_seed(7 * 1_000_003 + 2)
     assert torch.equal(initial_latents(7, 2, cfg), torch.randn((1, 4, 8, 8), generator=g))
+
+
+def test_interleave_ln_fold_matches_geglu_interleave():
+    """The LayerNorm fold's rows (folded weight, fp32 bias, row sums) are reordered exactly like interleave_geglu
+    reorders the projection's rows, so sdmoe_linear_geglu_ln sees the same [value 8 | gate 8] expert-major layout."""
+    from sdmoe import ops
+    F, K = 160, 64
+    g = torch.Generator().manual_seed(3)
+    w = torch.randn(2 * F, K, generator=g)
+    b = torch.randn(2 * F, generator=g)
+    perm = torch.randperm(F, generator=g)
+    fold = ops.LNFold.__new__(ops.LNFold)
+    fold.eps, fold.w, fold.bias, fold.wsum = 1e-5, w, b, w.sum(1)
+    il = ops.interleave_ln_fold(fold, perm)
+    w_il, b_il = ops.interleave_geglu(w, b, perm)
+    assert torch.equal(il.w, w_il) and torch.equal(il.bias, b_il)
+    assert torch.equal(il.wsum, w_il.sum(1))
+
+
+def test_conv_weight_with_shortcut_layout():
+    """[Cout, 9*Cin + Cin2]: conv2's implicit-GEMM K order first, then the 1x1 shortcut's input channels."""
+    from sdmoe import ops
+    Cout, Cin, Cin2 = 16, 64, 128
+    w = torch.randn(Cout, Cin // 64, 3, 3, 64)
+    ws = torch.randn(Cout, Cin2)
+    cat = ops.conv_weight_with_shortcut(w, ws)
+    assert cat.shape == (Cout, 9 * Cin + Cin2) and cat.is_contiguous()
+    assert torch.equal(cat[:, :9 * Cin], w.reshape(Cout, -1)) and torch.equal(cat[:, 9 * Cin:], ws)
+
+
+def test_sdmoe_tune_env_is_parsed_at_load(monkeypatch):
+    """SDMOE_TUNE="knob=value,..." applies sdmoe_tune at library load; a bad knob raises."""
+    from sdmoe import _lib
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setenv("SDMOE_TUNE", "1=0,0=0")
+    assert _lib.load() is not None
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setenv("SDMOE_TUNE", "99=1")
+    with pytest.raises(_lib.SdmoeError):
+        _lib.load()
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.delenv("SDMOE_TUNE")
+    _lib.load()
