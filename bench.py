@@ -61,17 +61,37 @@ def parse():
     p.add_argument("--cpu-full-image", action="store_true",
                    help="cpu_baseline: time one whole image (all inference steps of the oracle's DDIM+CFG loop, "
                         "several minutes) instead of the bounded cpu-evals sample")
+    p.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--traffic", type=str, default=os.path.join(ROOT, "profiles", "pmc_conv_traffic.json"),
                    help="PMC summary json from tools/pmc_traffic.py (HBM bytes per conv launch)")
     return p.parse_args()
 
 
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` without an external launcher: start N fresh worker processes (one per GPU) under
+    torch.distributed.run as a CHILD process -- this process has made no GPU call, and it does not exec -- and exit
+    with the workers' status. Rank 0's JSON line reaches stdout through the child's inherited stdout."""
+    import socket
+    import subprocess
+    with socket.socket() as s:  # a free port on the loopback interface for the rendezvous
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    print(f"[bench] launching {n} ranks: {' '.join(cmd[1:])}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
+
+
 def setup_dist(n):
     """One process per GPU over RCCL ("nccl"). SDMOE_SAME_DEVICE_REHEARSAL=1 (rehearsal of the N > 1 code path on a
-    one-GPU box, never used for a measurement): every rank on cuda:0, gloo collectives."""
+    one-GPU box, never used for a measurement): every rank on cuda:0, gloo collectives.
+    The process group must have exactly n ranks (`--gpus n`): a mismatch is an error, not a silent 1-GPU run."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != n:
+        raise SystemExit(f"bench.py: --gpus {n} but WORLD_SIZE={world}; launch with --nproc-per-node {n} (or run "
+                         f"`bench.py --gpus {n}` with no launcher and it starts the ranks itself)")
     if world > 1 and os.environ.get("SDMOE_SAME_DEVICE_REHEARSAL") == "1":
         local = 0
         torch.cuda.set_device(0)
@@ -274,8 +294,26 @@ def metric_label(args):
     return f"images/sec SD-1.4 512² {sched}, {mask}; 1→8 GPU scaling"
 
 
+def launch_probe(args):
+    """--launch-probe (CPU test of the launcher path, tests/test_distributed.py): each rank joins a gloo group, the
+    ranks all-reduce their rank ids, rank 0 prints the line bench.py would print its n_gpus from. No GPU call."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    dist.init_process_group("gloo")
+    t = torch.tensor([float(dist.get_rank())])
+    dist.all_reduce(t)
+    if dist.get_rank() == 0:
+        print(json.dumps({"probe": True, "n_gpus": dist.get_world_size(), "rank_sum": int(t.item())}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if args.launch_probe:
+        return launch_probe(args)
     if args.batch is None:
         args.batch = 2 if args.model == "sdxl" else 8
     world, rank, local = setup_dist(args.gpus)

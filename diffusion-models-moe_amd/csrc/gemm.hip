@@ -432,6 +432,7 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
       // fit a second register set. sched_barrier pins the read / MFMA order so hipcc cannot sink the reads to
       // their first use (which exposes the LDS latency every group).
       constexpr int NKK = BK / 32, NG = FM / 2;
+      static_assert(FM % 2 == 0, "the pipelined loop reads fragment rows in pairs");
       constexpr bool BDB = FN <= 5 && !KEEP;  // second B set: +4*FN VGPRs (the masked modes need those registers)
       half8 bcur[FN], bnxt[FN];
 #pragma unroll

@@ -60,8 +60,17 @@ class MultiConceptRemoverWanda:
 
     @staticmethod
     def stitch(before, after):
-        """[before | after] along the last (width) axis: the side-by-side pair of multi_concept_remover.py:83-99."""
-        return torch.cat([before, after], dim=-1)
+        """[before | after] side by side along the WIDTH axis: the pair of multi_concept_remover.py:83-99.
+        torch tensors are CHW (RGB, output_type 'pt') or latents [4, H, W]: width is the last axis. numpy arrays are
+        the pipeline's HWC images (output_type 'np'): width is axis -2. Anything else is refused."""
+        if isinstance(before, torch.Tensor) and isinstance(after, torch.Tensor):
+            return torch.cat([before, after], dim=-1)
+        if isinstance(before, np.ndarray) and isinstance(after, np.ndarray):
+            if before.ndim != 3:
+                raise ValueError(f"numpy images must be HWC, got shape {before.shape}")
+            return np.concatenate([before, after], axis=-2)
+        raise TypeError(f"cannot stitch {type(before).__name__} and {type(after).__name__}: expected two torch "
+                        f"tensors (CHW / latents) or two numpy HWC arrays")
 
     def remove_concepts(self, model, prompt, concepts):
         """Returns (stitched [original | union removed], per-concept stitched pairs or None) -- two values, as the

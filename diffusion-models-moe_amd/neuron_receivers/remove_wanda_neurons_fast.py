@@ -24,6 +24,8 @@ bit-identical (tests/test_gpu_wanda.py). Past the budget, or with bake_budget_by
 """
 from __future__ import annotations
 
+import weakref
+
 import numpy as np
 import torch
 
@@ -32,6 +34,16 @@ from sdmoe.unet import LoRACompatibleLinear
 
 from neuron_receivers.base_receiver import GEGLU
 from neuron_receivers.predictivity import NeuronPredictivity
+
+
+# HBM held by baked masked weights, per device, over EVERY receiver of the process (a MultiConceptRemoverWanda holds
+# one receiver per concept plus the union one: a per-instance count would let each bake its own budget's worth).
+# Entries are released by a finalizer when the baked tensor is freed.
+_BAKED_BYTES = {}
+
+
+def _baked_release(dev, nbytes):
+    _BAKED_BYTES[dev] = _BAKED_BYTES.get(dev, 0) - nbytes
 
 
 class WandaRemoveNeuronsFast(NeuronPredictivity):
@@ -54,7 +66,6 @@ class WandaRemoveNeuronsFast(NeuronPredictivity):
         self.layer = 0
         self.gates = []
         self._dev = {}
-        self._baked_bytes = 0
 
     @classmethod
     def from_packed(cls, seed, packed, T, n_layers, **kw):
@@ -65,10 +76,9 @@ class WandaRemoveNeuronsFast(NeuronPredictivity):
         obj.remove_timesteps, obj.weights_shape = None, None
         obj.mask_bits = {t: {l: np.asarray(packed[t][l], dtype=np.uint8) for l in range(n_layers)} for t in range(T)}
         obj.timestep, obj.layer, obj.gates, obj._dev = 0, 0, [], {}
-        obj._baked_bytes = 0
         return obj
 
-    bake_budget_bytes = 24 << 30  # HBM for baked masked weights (class default; 0 = always mask inside the GEMM)
+    bake_budget_bytes = 24 << 30  # HBM for baked masked weights, per device and process (0 = always mask in the GEMM)
 
     def dense_mask(self, t, l):
         bits = self.mask_bits[t][l]
@@ -78,9 +88,7 @@ class WandaRemoveNeuronsFast(NeuronPredictivity):
         self.mask_bits[t][l] = np.asarray(bits, dtype=np.uint8)
         # drop the device copy and every layout derived from it (K-major, permuted, GEGLU gate-half forms)
         for key in [k for k in self._dev if k == (t, l) or (isinstance(k[0], str) and tuple(k[1:3]) == (t, l))]:
-            if key[0] == "baked":
-                self._baked_bytes -= self._dev[key].numel() * 2
-            del self._dev[key]
+            del self._dev[key]  # a baked weight's HBM is returned to the budget by its finalizer
 
     def device_bits(self, t, l, device):
         d = self._dev.get((t, l))
@@ -90,27 +98,38 @@ class WandaRemoveNeuronsFast(NeuronPredictivity):
 
     def device_kmajor(self, t, l, device, perm=None):
         """The (t, l) mask in sdmoe_linear_masked's layout (int64 [4C/64, C]); perm (int32 device [4C], the routed
-        FFN's neuron order) permutes its columns. Converted once per (t, l, perm) on the device and cached."""
-        key = ("kmajor", t, l, None if perm is None else perm.data_ptr())
-        d = self._dev.get(key)
-        if d is None:
-            d = self._dev[key] = ops.wmask_kmajor(self.device_bits(t, l, device), perm)
-        return d
+        FFN's neuron order) permutes its columns. Converted once per (t, l, perm) on the device and cached. The cache
+        entry holds the perm tensor itself and is matched by identity (an address could be reused by a later
+        routing's perm after a re-MoE-fication); a new perm for the same (t, l) replaces the entry."""
+        key = ("kmajor", t, l, perm is None)
+        ent = self._dev.get(key)
+        if ent is None or ent[0] is not perm:
+            ent = self._dev[key] = (perm, ops.wmask_kmajor(self.device_bits(t, l, device), perm))
+        return ent[1]
 
     def baked_weight(self, t, l, weight, perm=None):
         """W * (1 - M[t][l]) (columns reordered by perm, int32 device [4C], if given), made once per (t, l, weight
-        version, perm) with sdmoe_mask_weight and kept in HBM; None when it would exceed bake_budget_bytes."""
-        key = ("baked", t, l, weight.data_ptr(), weight._version, None if perm is None else perm.data_ptr())
-        w = self._dev.get(key)
-        if w is None:
-            nbytes = weight.numel() * weight.element_size()
-            if self._baked_bytes + nbytes > self.bake_budget_bytes:
-                return None
-            w = ops.mask_weight(weight, self.device_bits(t, l, weight.device))
-            if perm is not None:
-                w = torch.index_select(w, 1, perm.long()).contiguous()
-            self._dev[key] = w
-            self._baked_bytes += nbytes
+        version, perm) with sdmoe_mask_weight and kept in HBM; None when it would exceed bake_budget_bytes (shared by
+        all receivers of the process on that device). The entry keeps references to the weight and perm it was made
+        from (so neither address can be recycled while it lives) and is replaced -- its HBM released -- when either
+        changes for the same (t, l)."""
+        key = ("baked", t, l, perm is None)
+        ent = self._dev.get(key)
+        if ent is not None and ent[0].data_ptr() == weight.data_ptr() and ent[1] == weight._version \
+                and ent[2] is perm:
+            return ent[3]
+        if ent is not None:
+            del self._dev[key]  # stale: evict before accounting the replacement
+        nbytes = weight.numel() * weight.element_size()
+        dev = str(weight.device)
+        if _BAKED_BYTES.get(dev, 0) + nbytes > self.bake_budget_bytes:
+            return None
+        w = ops.mask_weight(weight, self.device_bits(t, l, weight.device))
+        if perm is not None:
+            w = torch.index_select(w, 1, perm.long()).contiguous()
+        _BAKED_BYTES[dev] = _BAKED_BYTES.get(dev, 0) + nbytes
+        weakref.finalize(w, _baked_release, dev, nbytes)
+        self._dev[key] = (weight, weight._version, perm, w)
         return w
 
     def _check_shape(self, bits, weight, what):

@@ -186,9 +186,11 @@ class GEGLU(nn.Module):
             self._il_ln_key = key
         return self._il_ln
 
-    def routed(self, x, removed=None, want_gate=False, sel_out=None):
+    def routed(self, x, removed=None, want_gate=False, sel_out=None, score_out=None):
         """proj GEMM + routed GEGLU kernel. x: [..., C] fp16. Returns (out [..., 4C], masked gate or None).
-        sel_out (optional int32 [tokens, ceil(E/32)]) receives the per-token top-k expert bitmask.
+        sel_out (optional int32 [tokens, ceil(E/32)]) receives the per-token top-k expert bitmask, score_out
+        (optional fp16 [tokens, E]) the expert scores the top-k ranked (removed experts: 0 on the unfused path; their
+        raw gate sums on the fused path, where the removal is applied inside the top-k kernel).
 
         When the caller (FeedForward) allows it and the experts are balanced, the fused path runs instead:
         the projection GEMM's epilogue computes value*act(gate) and the expert scores, a small kernel applies
@@ -211,7 +213,8 @@ class GEGLU(nn.Module):
             if routing is None:
                 out = ops.linear_geglu(x2, w_il, b_il, act, ln=lnf)
             else:
-                score = torch.empty((x2.shape[0], routing.E), dtype=torch.float16, device=x.device)
+                score = score_out if score_out is not None else \
+                    torch.empty((x2.shape[0], routing.E), dtype=torch.float16, device=x.device)
                 out = ops.linear_geglu(x2, w_il, b_il, act, score=score, esize=routing.esize, ln=lnf)
                 if FUSED_KEEP and routing.F % 64 == 0:
                     # the dropped experts' neurons are zeroed by the down projection as it reads them
@@ -226,7 +229,8 @@ class GEGLU(nn.Module):
             x2 = ops.layernorm(x2, norm.weight, norm.bias, norm.eps)
         y = self.proj.run(x2)
         gate = torch.empty((x2.shape[0], self.inner_dim), dtype=torch.float16, device=x.device) if want_gate else None
-        out = ops.geglu_route(y, self.routing(), act_code(self.gelu), removed=removed, gate_out=gate, sel_out=sel_out)
+        out = ops.geglu_route(y, self.routing(), act_code(self.gelu), removed=removed, gate_out=gate, sel_out=sel_out,
+                              score_out=score_out)
         out = out.view(*shp[:-1], self.inner_dim)
         return out, (gate.view(*shp[:-1], self.inner_dim) if want_gate else None)
 
@@ -286,6 +290,18 @@ def _sole_receiver(module, method):
     return owner
 
 
+def _ln_safe_hook(module, owner):
+    """True when `module`'s one forward hook is exactly the function its receiver class marks LN-safe
+    (`_sdmoe_ln_safe_hook`: a hook_fn that only hands input[0] to GEGLU.routed(), which resolves a LayerNorm deferred
+    into the call). Compares the REGISTERED hook's function with the marker looked up on the class, so a subclass that
+    overrides hook_fn without re-marking it is not LN-safe."""
+    if owner is None:
+        return False
+    hooks = list(module._forward_hooks.values())
+    fn = getattr(hooks[0], "__func__", None) if len(hooks) == 1 else None
+    return fn is not None and fn is getattr(type(owner), "_sdmoe_ln_safe_hook", None)
+
+
 class FeedForward(nn.Module):
     def __init__(self, geglu, down):
         super().__init__()
@@ -316,8 +332,7 @@ class FeedForward(nn.Module):
         geglu._allow_permuted_out = (not dhooks or masker is not None) and (not geglu._forward_hooks or owner is not None)
         # ln (the block's norm3): deferred into the GEGLU projection when nothing but GEGLU's own methods can see
         # the module input (no hook, or one sdmoe receiver whose hook hands input[0] to routed()); else applied here
-        if ln is not None and geglu._forward_hooks and (
-                owner is None or getattr(type(owner), "hook_fn", None) is not getattr(owner, "_sdmoe_ln_safe_hook", 0)):
+        if ln is not None and geglu._forward_hooks and not _ln_safe_hook(geglu, owner):
             x2d = ops.layernorm(x2d, ln.weight, ln.bias, ln.eps)
             ln = None
         xv = x2d.view(nimg, -1, x2d.shape[1])

@@ -169,3 +169,29 @@ def test_data_parallel_pipeline_world2():
     assert off == 0
     for a, b in zip(imgs0 + imgs1, full):
         np.testing.assert_allclose(a, b.numpy(), rtol=1e-4, atol=1e-4)
+
+
+def test_bench_launcher_starts_n_ranks():
+    """`bench.py --gpus 2` with no external launcher starts 2 ranks itself (torch.distributed.run as a child
+    process); --launch-probe makes each rank join a gloo group instead of touching a GPU, and rank 0 reports the
+    group's size."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                             "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launch-probe"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert lines == [{"probe": True, "n_gpus": 2, "rank_sum": 1}], r.stdout
+
+
+def test_bench_refuses_world_size_mismatch():
+    """--gpus N inside a process group of another size is an error, never a silent 1-rank measurement."""
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launch-probe"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr

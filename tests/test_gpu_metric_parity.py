@@ -1,0 +1,267 @@
+"""Parity at the METRIC's configuration (BASELINE.json configs 2-4).
+
+1. Same-input expert selection at the bench's exact shapes. The bench's U-Net batch (SD-1.4 at 64x64 latents, 8
+   prompts -> U-Net batch 16 with CFG; relufied, top-k 0.2, expert 20, RemoveExperts removal for t < 20) runs 2
+   DDIM steps through observe_activation on the fused + keep routed FFN. Every hooked call records its input and
+   the device's per-token selection and scores. The reference hook (remove_skilled_experts.py:24-55, in fp16 on
+   the CPU as the reference's fp16 pipeline computes it: the CPU fp16 linear is an fp32 accumulation rounded
+   once) is re-run on exactly those inputs. So the trunk's fp16-vs-fp32 drift plays no part: the selection must
+   be identical on every row except
+     * exact ties at the k-th score, where torch.topk's order is implementation-defined: the device's choice must
+       be a valid top-k of the reference's scores (tie-consistent);
+     * rows whose k-th/(k+1)-th gap is within 2 fp16 ulps: our projection GEMM sums in another fp32 order, so a
+       y element can sit one ulp away and move a score by an ulp. Those flips are counted and reported.
+   At least 95 % of the rows must be compared. The same check runs for SDXL-base at 1024^2 (70 layers, E = 128 /
+   256) in tests/test_gpu_sdxl.py.
+2. The full 50-step trajectory: one prompt at 64x64, all 50 DDIM steps (so the t = 20 removal cut-off is crossed),
+   vs the fp32 oracle pipeline with the reference hook (fp16 routing, near-tie rows teacher-forced). Final latents
+   must agree to max-abs <= 2e-2 and PSNR >= 40 dB. Both latents are then decoded to 512^2 RGB, the
+   device's through the HIP VAE and the oracle's through the oracle VAE: pixel tolerance max-abs <= 2e-2 (on [0, 1])
+   and PSNR >= 40 dB.
+3. Config 4 at its real per-GPU shard: the union Wanda mask + MoE routing at 64x64 latents, 2 prompts, 2 steps,
+   with the same-input selection check of 1 and the trunk vs the oracle.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from sdmoe.config import UNetConfig  # noqa: E402
+from sdmoe.unet import UNet2DConditionModel  # noqa: E402
+from sdmoe.weights import make_state_dict  # noqa: E402
+from sdmoe.pipeline import StableDiffusionPipeline  # noqa: E402
+from oracle import hooks_ref as H  # noqa: E402
+
+from test_gpu_unet import DEV, rel_l2, sel_bits_to_bool, recording, forced_factory, run_oracle  # noqa: E402
+
+
+def psnr(got, ref, peak=None):
+    got, ref = got.double(), ref.double()
+    mse = ((got - ref) ** 2).mean().item()
+    peak = (ref.max() - ref.min()).item() if peak is None else peak
+    return float("inf") if mse == 0 else 10 * np.log10(peak * peak / mse)
+
+
+def same_input_recorder(cls):
+    """Receiver subclass recording every hooked call's (t, l, input rows, device selection bits, device scores).
+    It routes exactly as cls.hook_fn (same removal lookup, same fused path); only sel_out/score_out are added."""
+    class Rec(cls):
+        def hook_fn(self, module, input, output):
+            x = input[0]
+            E = module.patterns.shape[0]
+            rows = x.numel() // x.shape[-1]
+            sel = torch.zeros((rows, (E + 31) // 32), dtype=torch.int32, device=x.device)
+            score = torch.empty((rows, E), dtype=torch.float16, device=x.device)
+            t, l = self.timestep, self.layer
+            removed = self.removed_for(module, t, l) if module.patterns is not None else None
+            out, _ = module.routed(x, removed=removed, sel_out=sel, score_out=score)
+            self.update_time_layer()
+            self.records.append((t, l, x.detach().reshape(rows, -1).cpu(), sel.cpu(), score.cpu()))
+            return out
+        _sdmoe_ln_safe_hook = hook_fn
+    return Rec
+
+
+def check_same_input(records, mods, lists, act, min_compared=0.95):
+    """Re-run the reference hook (fp16 CPU) on each recorded input; see the module docstring for the contract.
+    Returns the counts (asserting the contract as it goes)."""
+    tot = dict(rows=0, compared=0, clear=0, exact_tie=0, tie_consistent=0, near_tie=0, near_tie_flips=0,
+               score_bit_equal_rows=0, calls=0)
+    weights = {}
+    for t, l, x, sel_bits, dscore in records:
+        m = mods[l]
+        if l not in weights:
+            weights[l] = (m.proj.weight.detach().cpu(), m.proj.bias.detach().cpu(),
+                          H.patterns_from_labels(m.labels.numpy(), torch.float16), m.k)
+        w, b, P, k = weights[l]
+        E = P.shape[0]
+        ids = lists[t][l]
+        removing = bool(ids) and t < 20
+        y = F.linear(x, w, b)                         # the hook's projection (moefy.py:12), fp16 as the reference
+        h, g = y.chunk(2, dim=-1)
+        g = H.act_fn(act)(g)
+        Pm = P.clone()
+        if removing:
+            Pm[list(ids), :] = 0                      # remove_skilled_experts.py:31-33
+        so = H.expert_scores(g, Pm).float().numpy()   # :45
+        sd = dscore.float().numpy()
+        if removing:
+            sd[:, list(ids)] = 0                      # the fused path reports removed experts' raw sums
+        dev = sel_bits_to_bool(sel_bits, E).numpy()
+        ref = H.topk_lowest_index(torch.from_numpy(so), k).numpy()
+        s = np.sort(so, axis=1)[:, ::-1]
+        vk, vk1 = s[:, k - 1], s[:, k]
+        tie = vk == vk1
+        ulp = np.spacing(np.abs(vk).astype(np.float16)).astype(np.float32)
+        near = ~tie & (vk - vk1 <= 2 * ulp)
+        clear = ~tie & ~near
+        mism = (dev != ref).any(1)
+        assert (dev.sum(1) == k).all(), (t, l)
+        assert not mism[clear].any(), f"(t={t}, l={l}): selection differs on {int(mism[clear].sum())} clear rows"
+        # tie rows: every selected expert scores >= the k-th value, every other one <= it (reference's scores)
+        sel_min = np.where(dev, so, np.inf).min(1)
+        uns_max = np.where(~dev, so, -np.inf).max(1)
+        consistent = (sel_min >= vk) & (uns_max <= vk)
+        score_eq = (so == sd).all(1)
+        # a tie row may only be inconsistent where the device's own scores differ from the reference's
+        assert not (tie & ~consistent & score_eq).any(), (t, l)
+        tot["rows"] += tie.size
+        tot["calls"] += 1
+        tot["clear"] += int(clear.sum())
+        tot["exact_tie"] += int(tie.sum())
+        tot["tie_consistent"] += int((tie & consistent).sum())
+        tot["near_tie"] += int(near.sum())
+        tot["near_tie_flips"] += int((near & mism).sum())
+        tot["score_bit_equal_rows"] += int(score_eq.sum())
+        tot["compared"] += int(clear.sum() + (tie & consistent).sum())
+    assert tot["compared"] >= min_compared * tot["rows"], tot
+    return tot
+
+
+def sd14_pipe(size, seed, steps):
+    from moefication.helper import moefy_synthetic
+    from sparsity.relufy_model import find_and_change_geglu
+    cfg = UNetConfig.sd14(size)
+    sd = make_state_dict(cfg, seed)
+    pipe = StableDiffusionPipeline(UNet2DConditionModel.from_state_dict(sd, cfg, DEV), DEV, num_inference_steps=steps)
+    find_and_change_geglu(pipe.unet)               # relufied (config 2)
+    moefy_synthetic(pipe, 0.2, 20, seed=seed + 1)  # E = 4C/20, k = int(0.2 E)
+    mods = [m for n, m in pipe.unet.named_modules() if n.endswith("ff.net.0")]
+    return cfg, sd, pipe, mods
+
+
+def removal_lists(mods, T, seed):
+    g = torch.Generator().manual_seed(seed)
+    return {t: {l: sorted(torch.randperm(m.patterns.shape[0], generator=g)[:m.patterns.shape[0] // 10].tolist())
+                for l, m in enumerate(mods)} for t in range(T)}
+
+
+def test_same_input_selection_sd14_64x64_batch16(parity_report):
+    """Part 1 of the module docstring at the bench's workload: 8 prompts (U-Net batch 16), 2 DDIM steps."""
+    from neuron_receivers import RemoveExperts
+    from conftest import heartbeat
+    cfg, sd, pipe, mods = sd14_pipe(64, 41, 2)
+    del sd
+    L, T = len(mods), 2
+    lists = removal_lists(mods, T, 42)
+    rec = same_input_recorder(RemoveExperts)(0, None, T, L, expert_indices=lists, store_gates=False)
+    rec.records = []
+    prompts = [f"synthetic prompt {i}" for i in range(8)]
+    out, _ = rec.observe_activation(pipe, prompts)
+    torch.cuda.synchronize()
+    assert (rec.timestep, rec.layer) == (T, 0) and len(rec.records) == T * L
+    assert all(m._out_keep is not None for m in mods), "fused + keep path did not run"
+    assert rec.records[0][2].shape[0] == 16 * 4096
+    with heartbeat("same-input sd14 64x64 b16"):
+        tot = check_same_input(rec.records, mods, lists, "relu")
+    parity_report("same_input_selection_sd14_64x64_b16_remove_relu", **tot)
+
+
+def test_trajectory_50_steps_sd14_64x64(parity_report):
+    """Part 2 of the module docstring: one prompt, all 50 DDIM steps, latents and decoded pixels vs the oracle."""
+    from neuron_receivers import RemoveExperts
+    from oracle.unet_ref import UNetRef
+    from oracle import vae_ref
+    from sdmoe.vae import AutoencoderKLDecoder, VAEConfig, make_vae_state_dict, postprocess
+    from conftest import heartbeat
+    steps = 50
+    cfg, sd, pipe, mods = sd14_pipe(64, 51, steps)
+    L = len(mods)
+    layers = [(m.labels.numpy(), m.patterns.shape[0], m.k) for m in mods]
+    lists = removal_lists(mods, steps, 52)  # removal applies at t < 20 only (remove_skilled_experts.py:32)
+    rec = recording(RemoveExperts)(0, None, steps, L, expert_indices=lists, store_gates=False)
+    rec.sels = []
+    prompts = ["Starry night by Van Gogh"]
+    out, _ = rec.observe_activation(pipe, prompts)
+    torch.cuda.synchronize()
+    assert (rec.timestep, rec.layer) == (steps, 0) and len(rec.sels) == steps * L
+    got = out[0].float().cpu()
+    vcfg = VAEConfig.sd14()
+    vsd = make_vae_state_dict(vcfg, 0)
+    vae = AutoencoderKLDecoder(vsd, vcfg, DEV)
+    pix_dev = postprocess(vae.decode(out[0][None].float())).cpu()
+    del pipe, vae
+    torch.cuda.empty_cache()
+    ref = UNetRef({k: v.half().float() for k, v in sd.items()}, cfg)
+    del sd
+    stats = dict(rows=0, clear=0, clear_mismatch=0, forced=0)
+    with heartbeat("trajectory-50 oracle"):
+        exp = run_oracle(ref, cfg, prompts, steps,
+                         ff_hook_factory=forced_factory(layers, "relu", rec.sels, lists, stats))[0]
+    with heartbeat("trajectory-50 oracle vae"):
+        vsd16 = {k: v.half().float() for k, v in vsd.items()}
+        pix_ref = postprocess(vae_ref.decode(vsd16, vcfg, exp[None]))
+    err = (got - exp).abs().max().item()
+    p_lat = psnr(got, exp)
+    perr = (pix_dev - pix_ref).abs().max().item()
+    p_pix = psnr(pix_dev, pix_ref, peak=1.0)
+    parity_report("trajectory_50_ddim_sd14_64x64_remove_relu", rows=stats["rows"], clear=stats["clear"],
+                  flips=stats["forced"], clear_mismatch=stats["clear_mismatch"], latent_max_abs=err,
+                  latent_psnr_db=p_lat, latent_rel_l2=rel_l2(got, exp), pixel_max_abs=perr, pixel_psnr_db=p_pix,
+                  latent_absmax=exp.abs().max().item())
+    assert torch.isfinite(got).all()
+    assert err <= 2e-2 and p_lat >= 40.0, (err, p_lat)
+    assert perr <= 2e-2 and p_pix >= 40.0, (perr, p_pix)
+
+
+def test_union_wanda_moe_sd14_64x64(parity_report):
+    """Part 3 of the module docstring (config 4: multi_concept_remover.py:43-53 -> remove_wanda_neurons_fast.py:
+    69-83 on top of RemoveExperts routing): 2 prompts, 2 DDIM steps at 64x64, union of two concepts' Wanda masks
+    (baked per (t, l) in the experts' column order, the bench's default)."""
+    from neuron_receivers import RemoveExperts, WandaRemoveNeuronsFast, MultiConceptRemoverWanda
+    from oracle.unet_ref import UNetRef
+    from conftest import heartbeat
+    cfg, sd, pipe, mods = sd14_pipe(64, 61, 2)
+    downs = [m for n, m in pipe.unet.named_modules() if n.endswith("ff.net.2")]
+    L, T = len(mods), 2
+    rng = np.random.default_rng(62)
+    concepts = {c: {t: {l: (rng.random(tuple(downs[l].weight.shape)) < 0.025).astype(np.int64) for l in range(L)}
+                    for t in range(T)} for c in ("van gogh", "monet")}
+    removers = {c: WandaRemoveNeuronsFast(0, None, T, L, masks=m, store_gates=False) for c, m in concepts.items()}
+    mc = MultiConceptRemoverWanda(None, 0, T, L, concepts_to_remove=list(concepts), removers=removers)
+    mc.reset_union_remover()
+    mc.handle_multiple_concepts(list(concepts))
+    union = {t: {l: H.union_masks([concepts[c][t][l] for c in concepts]) for l in range(L)} for t in range(T)}
+    wanda = mc.union_neuron_remover
+    lists = removal_lists(mods, T, 63)
+    rec = same_input_recorder(RemoveExperts)(0, None, T, L, expert_indices=lists, store_gates=False)
+    rec.records = []
+    prompts = ["a church in the style of van gogh", "water lilies"]
+    wanda.reset_time_layer()
+    wanda.prepare(pipe)
+    hooks = wanda.register_hooks(pipe)
+    try:
+        out, _ = rec.observe_activation(pipe, prompts)
+    finally:
+        wanda.remove_hooks(hooks)
+    torch.cuda.synchronize()
+    assert (wanda.timestep, wanda.layer) == (T, 0) and (rec.timestep, rec.layer) == (T, 0)
+    assert all(m._out_keep is not None for m in mods), "fused routed path did not run under the Wanda hook"
+    assert any(k[0] == "baked" and k[3] is False for k in wanda._dev if isinstance(k[0], str))
+    got = torch.stack(out).float().cpu()
+    with heartbeat("union 64x64 same-input"):
+        tot = check_same_input(rec.records, mods, lists, "relu")
+    # the trunk vs the oracle, with the device's selection teacher-forced on every row (selection itself was
+    # checked above on the device's own hook inputs)
+    sels = [sel_bits_to_bool(sb, mods[l].patterns.shape[0]) for t, l, _, sb, _ in rec.records]
+    rec.records = None
+    del pipe
+    torch.cuda.empty_cache()
+    layers = [(m.labels.numpy(), m.patterns.shape[0], m.k) for m in mods]
+    ref = UNetRef({k: v.half().float() for k, v in sd.items()}, cfg)
+    del sd
+
+    def down_factory(step):
+        def hook(layer, x, w, b):
+            return H.wanda_linear(x, w, b, union[step][layer])
+        return hook
+    stats = dict(rows=0, clear=0, clear_mismatch=0, forced=0)
+    with heartbeat("union 64x64 oracle"):
+        exp = run_oracle(ref, cfg, prompts, T, ff_hook_factory=forced_factory(layers, "relu", sels, lists, stats),
+                         down_hook_factory=down_factory)
+    parity_report("union_wanda_moe_sd14_64x64", **tot, trunk_rel_l2=rel_l2(got, exp),
+                  trunk_clear_mismatch=stats["clear_mismatch"])
+    assert stats["clear_mismatch"] == 0, stats
+    assert rel_l2(got, exp) <= 1e-2

@@ -169,9 +169,9 @@ def test_union_wanda_moe_pipeline_sd14(bake, parity_report):
     assert (wanda.timestep, wanda.layer) == (2, 0) and (rec.timestep, rec.layer) == (2, 0)
     assert all(m._out_keep is not None for m in mods), "fused routed path did not run under the Wanda hook"
     if bake:  # the masked weight baked once per (t, l) in the experts' column order
-        assert any(k[0] == "baked" and k[5] is not None for k in wanda._dev if isinstance(k[0], str))
+        assert any(k[0] == "baked" and k[3] is False for k in wanda._dev if isinstance(k[0], str))
     else:     # the mask's permuted K-major form applied inside the GEMM
-        assert any(k[0] == "kmajor" and k[3] is not None for k in wanda._dev if isinstance(k[0], str))
+        assert any(k[0] == "kmajor" and k[3] is False for k in wanda._dev if isinstance(k[0], str))
     got = torch.stack(out).float().cpu()
     ref = UNetRef({k: v.half().float() for k, v in sd.items()}, cfg)
 
@@ -190,3 +190,63 @@ def test_union_wanda_moe_pipeline_sd14(bake, parity_report):
     rec2 = RemoveExperts(0, None, T, L, replace_fn=GEGLU, expert_indices=lists, store_gates=False)
     out2, _ = rec2.observe_activation(pipe, prompts)
     assert rel_l2(torch.stack(out2).float().cpu(), got) > 1e-3
+
+
+@pytest.mark.parametrize("bake", [True, False], ids=["baked", "in_gemm"])
+def test_union_wanda_receiver_survives_remoefication(bake):
+    """One Wanda receiver reused across a re-MoE-fication with NEW expert labels (so a new Routing and a new neuron
+    permutation, possibly at a recycled device address): its cached permuted masks / baked weights must follow the
+    new permutation. The second run equals a fresh receiver's run bit for bit, and differs from the first run."""
+    from moefication.helper import moefy_synthetic
+    from sparsity.relufy_model import find_and_change_geglu
+    from neuron_receivers import MOEFy, WandaRemoveNeuronsFast
+    from neuron_receivers import remove_wanda_neurons_fast as W
+    from sdmoe.config import UNetConfig
+    from sdmoe.unet import UNet2DConditionModel
+    from sdmoe.weights import make_state_dict
+    from sdmoe.pipeline import StableDiffusionPipeline
+
+    cfg = UNetConfig.sd14(16)
+    pipe = StableDiffusionPipeline(UNet2DConditionModel.from_state_dict(make_state_dict(cfg, 31), cfg, DEV), DEV,
+                                   num_inference_steps=2)
+    find_and_change_geglu(pipe.unet)
+    downs = [m for n, m in pipe.unet.named_modules() if n.endswith("ff.net.2")]
+    T, L = 2, 16
+    rng = np.random.default_rng(32)
+    masks = {t: {l: (rng.random(tuple(downs[l].weight.shape)) < 0.05).astype(np.int64) for l in range(L)}
+             for t in range(T)}
+
+    def make():
+        w = WandaRemoveNeuronsFast(0, None, T, L, masks=masks, store_gates=False)
+        if not bake:
+            w.bake_budget_bytes = 0
+        return w
+
+    def run(wanda):
+        wanda.reset_time_layer()
+        wanda.prepare(pipe)
+        hooks = wanda.register_hooks(pipe)
+        try:
+            out, _ = MOEFy(seed=0, store_gates=False).observe_activation(pipe, ["a lighthouse"])
+        finally:
+            wanda.remove_hooks(hooks)
+        return out[0].clone()
+
+    reused = make()
+    moefy_synthetic(pipe, 0.2, 20, seed=1)
+    first = run(reused)
+    baked0 = W._BAKED_BYTES.get(str(downs[0].weight.device), 0)
+    moefy_synthetic(pipe, 0.2, 20, seed=2)  # new labels -> new Routing / perm for every layer
+    torch.cuda.empty_cache()
+    second = run(reused)
+    fresh = run(make())
+    assert torch.equal(second, fresh)
+    assert not torch.equal(first, second)
+    # stale permuted entries were replaced, not accumulated: one entry per (t, l) and form
+    forms = [k for k in reused._dev if isinstance(k[0], str)]
+    assert len(forms) == len(set(forms)) == T * L
+    if bake:
+        del reused, fresh
+        import gc
+        gc.collect()
+        assert W._BAKED_BYTES.get(str(downs[0].weight.device), 0) <= baked0
