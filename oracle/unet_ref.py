@@ -14,6 +14,7 @@ Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline may import this
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -31,9 +32,15 @@ def timestep_embedding(t, dim, flip_sin_to_cos=True, freq_shift=0.0, max_period=
     return emb
 
 
+# conv operands in channels_last (NHWC): the CPU (oneDNN) conv runs several times faster on NHWC operands than on NCHW
+# ones at these widths; the layout changes only the fp32 summation order. SDMOE_ORACLE_NHWC=0: plain NCHW.
+NHWC = os.environ.get("SDMOE_ORACLE_NHWC", "1") != "0"
+
+
 class UNetRef:
     def __init__(self, sd, cfg):
-        self.sd = {k: v.float() for k, v in sd.items()}
+        self.sd = {k: (v.float().contiguous(memory_format=torch.channels_last) if v.dim() == 4 and NHWC else v.float())
+                   for k, v in sd.items()}
         self.cfg = cfg
         self.layer = 0
 
@@ -42,7 +49,10 @@ class UNetRef:
         return F.linear(x, self.sd[name + ".weight"], self.sd.get(name + ".bias") if bias else None)
 
     def conv(self, x, name, stride=1, padding=1):
-        return F.conv2d(x, self.sd[name + ".weight"], self.sd[name + ".bias"], stride=stride, padding=padding)
+        if not NHWC:
+            return F.conv2d(x, self.sd[name + ".weight"], self.sd[name + ".bias"], stride=stride, padding=padding)
+        return F.conv2d(x.contiguous(memory_format=torch.channels_last), self.sd[name + ".weight"],
+                        self.sd[name + ".bias"], stride=stride, padding=padding).contiguous()
 
     def gn(self, x, name, eps):
         return F.group_norm(x, self.cfg.norm_num_groups, self.sd[name + ".weight"], self.sd[name + ".bias"], eps)

@@ -67,6 +67,8 @@ def check_out(o, ro, g, rg, h, rows):
     """On `rows`: the activated gate equals the reference's up to 3 fp16 ulps (see module docstring; < 3 % of
     elements differ at all), and the output is bit-identical wherever the gate is, otherwise within
     |value| * |gate diff| + ulp(out) (the product's exact propagation of that gate difference)."""
+    if not np.any(rows):
+        return
     o, ro, g, rg, h = (a[rows].astype(np.float32) for a in (o, ro, g, rg, h))
     gd = np.abs(g - rg)
     sp = fp16_spacing(np.maximum(np.abs(g), np.abs(rg)))

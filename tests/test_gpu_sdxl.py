@@ -135,37 +135,48 @@ def test_pipeline_remove_experts_sdxl_base_128x128(parity_report):
     """BASELINE config 5 at its real shape: the SDXL-base U-Net at 1024^2 (4x128x128 latents: 4096-token d=64
     self-attention at the 64x64 level, 10-deep transformers at 32x32), MoE-fied as the config-5 bench runs it (relufied,
     top-k 0.2, expert 20 -> E = 128 / 256 on 70 FFNs), RemoveExperts skilled-expert mask (t < 20), one DDIM step with
-    CFG (U-Net batch 2) through the fused + keep routed FFN, against the fp32 oracle with the reference hooks (fp16
-    routing, near-tie rows teacher-forced): selection identical on every clear row, latents rel L2 <= 1e-2."""
+    CFG (U-Net batch 2) through the fused + keep routed FFN.
+    (1) Same-input selection (test_gpu_metric_parity's contract): every one of the 70 hooked calls re-run by the
+        reference hook (fp16, CPU) on the device's own hook input: identical selection on every clear row and every
+        row with bit-equal scores, tie rows tie-consistent, >= 95 % of the rows compared.
+    (2) The trunk vs the fp32 oracle with the device's selection teacher-forced: latents rel L2 <= 1e-2."""
     from neuron_receivers import GEGLU, RemoveExperts
     from conftest import heartbeat
+    from test_gpu_metric_parity import same_input_recorder, check_same_input, teacher_forced_factory
+    from test_gpu_unet import sel_bits_to_bool
     cfg = UNetConfig.sdxl(128)
     with heartbeat("sdxl-128 weights"):
         unet, ref = build_rounded(cfg, seed=7)
     pipe = StableDiffusionPipeline(unet, DEV, num_inference_steps=1)
     layers = moefy_tiny(pipe, topk=0.2, expert_size=20, relu=True)
+    mods = [m for n, m in pipe.unet.named_modules() if n.endswith("ff.net.0")]
     L = len(layers)
     assert L == 70 and {E for _, E, _ in layers} == {128, 256}
     g = torch.Generator().manual_seed(13)
     lists = {0: {l: sorted(torch.randperm(layers[l][1], generator=g)[:layers[l][1] // 10].tolist()) for l in range(L)}}
-    rec = recording(RemoveExperts)(0, None, 1, L, replace_fn=GEGLU, expert_indices=lists, store_gates=False)
-    rec.sels = []
+    rec = same_input_recorder(RemoveExperts)(0, None, 1, L, replace_fn=GEGLU, expert_indices=lists, store_gates=False)
+    rec.records = []
     prompts = ["a photograph of an astronaut riding a horse"]
     out, _ = rec.observe_activation(pipe, prompts)
     torch.cuda.synchronize()
-    assert (rec.timestep, rec.layer) == (1, 0)
-    mods = [m for n, m in pipe.unet.named_modules() if n.endswith("ff.net.0")]
+    assert (rec.timestep, rec.layer) == (1, 0) and len(rec.records) == L
     assert all(m._out_keep is not None for m in mods), "fused routed path did not run"
     got = torch.stack(out).float().cpu()
     assert torch.isfinite(got).all()
+    with heartbeat("sdxl-128 same-input"):
+        check_same_input(rec.records, mods, lists, "relu",
+                         report=lambda **tot: parity_report("same_input_selection_sdxl_base_128x128", **tot))
+    sels = [sel_bits_to_bool(sb, mods[l].patterns.shape[0]) for t, l, _, sb, _ in rec.records]
+    rec.records = None
+    del pipe, unet, mods
+    torch.cuda.empty_cache()
     lat = torch.cat([initial_latents(0, i, cfg) for i in range(len(prompts))])
     ctx, ac = xl_inputs(cfg, prompts)
     B = len(prompts)
-    stats = dict(rows=0, clear=0, clear_mismatch=0, forced=0)
+    stats = dict(rows=0, clear=0, clear_disagree=0)
     with heartbeat("sdxl-128 oracle"):
         exp = denoise(ref, lat, ctx[:B], ctx[B:], num_inference_steps=1, added_cond=ac,
-                      ff_hook_factory=forced_factory(layers, "relu", rec.sels, lists, stats))
+                      ff_hook_factory=teacher_forced_factory(layers, "relu", sels, lists, stats))
     parity_report("pipeline_sdxl_base_128x128_remove_experts", rows=stats["rows"], clear=stats["clear"],
-                  near_tie=stats["rows"] - stats["clear"], flips=stats["forced"], rel_l2=rel_l2(got, exp))
-    assert stats["clear_mismatch"] == 0, stats
+                  oracle_trunk_clear_disagree=stats["clear_disagree"], rel_l2=rel_l2(got, exp))
     assert rel_l2(got, exp) <= 1e-2
