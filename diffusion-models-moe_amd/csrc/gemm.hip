@@ -36,6 +36,7 @@ int g_stages = 0;
 int g_tile = 0;
 int g_bk = 0;
 int g_prio = 0;
+int g_res16 = 1;  // knob 8: 1 = residual epilogues on the fp16 staging path (residual added in the copy-out), 0 = fp32
 int g_diag = 0;  // knob 6, diagnostics only (results garbage): bit 0 = no K-loop operand loads, bit 1 = no MFMAs,
                  // bit 2 = no epilogue (nothing stored), bit 3 = epilogue without its global stores
 
@@ -62,6 +63,7 @@ struct GemmParams {
   half_t* score; long ld_score;
   int esize;
   int prio;  // experiment knob: raise wave priority around the MFMA block
+  int res16;  // residual on the fp16 staging path (sdmoe_tune knob 8)
   int diag;  // diagnostic knob (sdmoe_tune 6): bit 0 skips the K-loop loads, bit 1 the MFMAs
   // expert keep mask of the A operand (MODE_KEEP / MODE_KEEPW): keep[(k / 64) * M * 8 + m * 8 + (k % 64) / 8] bit
   // (k % 8) = neuron k of token m survives the top-k; the A fragments are ANDed with it after their LDS read
@@ -84,6 +86,7 @@ struct GemmParams {
 };
 
 SDMOE_DEV int swz(int row) { return (row >> 1) & 7; }
+SDMOE_DEV bool g_res16_dev(const GemmParams& p) { return p.res16 != 0; }
 
 constexpr unsigned OOB = 0x80000000u;  // > every num_records used here (tensors < 2 GiB)
 
@@ -551,7 +554,7 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
   }
   __syncthreads();
   constexpr int CPR = WN / 8;
-  if (!GEGLU && p.act == ACT_NONE && !p.R) {
+  if (!GEGLU && p.act == ACT_NONE && (!p.R || g_res16_dev(p))) {
     // fp16 path: bias and per-image column add in registers on each lane's 4-column row piece (one rounding, as
     // epilogue8), staged as fp16 (one ds_write_b64 per fragment: 1/2.5 of the LDS time of staging fp32 with 4
     // ds_write_b32), then copied out in 16-B row chunks: 175 -> 166 us for the M = 65536, N = 2560, K = 320 linear,
@@ -565,8 +568,24 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
       b4[j] = (!LN && p.bias && n < p.N) ? *reinterpret_cast<const half4*>(p.bias + n) : (half4){0, 0, 0, 0};
     }
     half_t* st = reinterpret_cast<half_t*>(smem) + wave * (WM / NPASS16) * RS16;
+    // residual (fp16, 16-B row chunks): this pass's chunks are loaded before its accumulators are staged, so their
+    // latency hides behind the staging; added to the staged fp16 output in the copy-out (the output is rounded to
+    // fp16 and the residual added in fp16 arithmetic -- diffusers' fp16 `to_out(x) + hidden_states`)
+    constexpr int NCH16 = (WM / NPASS16) * CPR, NIT16 = (NCH16 + 63) / 64;
+    const bool res = p.R != nullptr;
 #pragma unroll
     for (int h = 0; h < NPASS16; ++h) {
+      half8 rr[NIT16];
+      if (res) {
+#pragma unroll
+        for (int it = 0; it < NIT16; ++it) {
+          const int id = lane + 64 * it;
+          const int r = id / CPR, c8 = id - r * CPR;
+          const int m = mw + h * (WM / NPASS16) + r, n = nw + c8 * 8;
+          rr[it] = (id < NCH16 && m < p.M && n < p.N) ? *reinterpret_cast<const half8*>(p.R + (long)m * p.ldr + n)
+                                                      : (half8){0, 0, 0, 0, 0, 0, 0, 0};
+        }
+      }
 #pragma unroll
       for (int i = 0; i < FM / NPASS16; ++i) {
         // one fragment row at a time: keeps the hoisted bias / column-add / residual loads to FN pieces (the 8-wave
@@ -607,11 +626,17 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      for (int id = lane; id < (WM / NPASS16) * CPR; id += 64) {
+#pragma unroll
+      for (int it = 0; it < NIT16; ++it) {
+        const int id = lane + 64 * it;
         const int r = id / CPR, c8 = id - r * CPR;
         const int m = mw + h * (WM / NPASS16) + r, n = nw + c8 * 8;
-        if (m >= p.M || n >= p.N) continue;
-        const half8 o = *reinterpret_cast<const half8*>(st + r * RS16 + c8 * 8);
+        if (id >= NCH16 || m >= p.M || n >= p.N) continue;
+        half8 o = *reinterpret_cast<const half8*>(st + r * RS16 + c8 * 8);
+        if (res) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = (half_t)((float)o[j] + (float)rr[it][j]);
+        }
         if (p.diag & 8) asm volatile("" ::"v"(o));
         else *reinterpret_cast<half8*>(p.C + (long)m * p.ldc + n) = o;
       }
@@ -779,6 +804,7 @@ int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
   p.part = p.ksplit > 1 ? ws : nullptr;
   p.prio = g_prio;
   p.diag = g_diag;
+  p.res16 = g_res16;
   const dim3 grid(ntiles * p.ksplit);
   {
     // 64-deep K-steps (a 32-deep 4/5-stage ring measured slower on every shape; the kernel is generic in BK).
@@ -1185,13 +1211,16 @@ extern "C" int sdmoe_mask_weight(const void* W, const void* bits, long N, long K
 }
 
 int sdmoe_attn_set_nqf(int v);  // attention.hip
+int sdmoe_gn_set_fused(int v);  // norm.hip
 
 extern "C" int sdmoe_tune(int knob, int value) {
   if (knob == 4) return sdmoe_attn_set_nqf(value);
+  if (knob == 7) return sdmoe_gn_set_fused(value);
   if (knob == 0 && (value == 0 || value == 2 || value == 3)) { g_stages = value; return SDMOE_OK; }
   if (knob == 1 && value >= 0 && value <= 6) { g_tile = value; return SDMOE_OK; }
   if (knob == 2 && (value == 0 || value == 32 || value == 64)) { g_bk = value; return SDMOE_OK; }
   if (knob == 3 && (value == 0 || value == 1)) { g_prio = value; return SDMOE_OK; }
   if (knob == 6 && value >= 0 && value <= 15) { g_diag = value; return SDMOE_OK; }
+  if (knob == 8 && (value == 0 || value == 1)) { g_res16 = value; return SDMOE_OK; }
   return SDMOE_EARG;
 }

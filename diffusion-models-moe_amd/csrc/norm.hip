@@ -12,6 +12,21 @@
 namespace {
 
 constexpr int GN_SMALL_HW = 1024;  // latents up to 32x32 take the single-launch path (measured crossover)
+int g_gn_fused = 1;  // sdmoe_tune knob 7: 1 = gn_fused_kernel for HW <= GN_FUSED_HW (sdmoe_groupnorm), 0 = two launches
+// single-launch statistics + apply up to 16x16 latents: 13.0 vs 15.9 us at 8x8 (C = 1280, 16 images), 14.5 vs 16.0
+// at 16x16; at 32x32 it is slower (21.9 vs 21.1 us, C = 640; 47.6 vs 42.2 at C = 1920): every block re-reads its
+// chunk's 1024 rows with 16 KB in flight, which no longer hides behind the saved launch (tools/micro_ab.py gn)
+constexpr int GN_FUSED_HW = 256;
+
+// chunk width of the small-latent kernels: whole groups and whole 16-B chunks (lcm(cpg, 8)), doubled towards 80
+// channels while the chunk count stays integral; 0 when no such chunk exists
+int gn_chunk_width(int C, int groups) {
+  const int cpg = C / groups;
+  int wc = cpg;
+  while (wc % 8) wc += cpg;
+  while (wc < 80 && C % (2 * wc) == 0 && 2 * wc <= 256) wc *= 2;
+  return (wc <= 256 && wc / cpg <= 32 && C % wc == 0) ? wc : 0;
+}
 
 // Partial sums of (x - ref) and (x - ref)^2 over a slice of rows of one image, for every group at once.
 // ref = first element of the group in the image's row 0 (shifted sums keep the variance well conditioned).
@@ -156,6 +171,105 @@ __global__ __launch_bounds__(256) void gn_small_kernel(const half_t* __restrict_
   }
 }
 
+// GroupNorm statistics AND apply(+SiLU) in ONE launch for small latents (HW <= GN_FUSED_HW). Block (chunk, slice, image):
+// the statistics of its (image, WC-channel chunk) exactly as gn_small_kernel computes them (same shifted sums, same
+// reduction order, same fp64 finalize -> bit-identical scale/shift), every block over ALL HW rows of its chunk (the
+// S slices of a chunk re-read it from L2: S x the chunk's bytes, a few MB), then the apply on its own slice of rows.
+// Replaces gn_small_kernel + gn_apply_kernel -- two dependent launches of ~10 us each on these 0.1-1.3 MB
+// tensors, i.e. launch and load latency, not bytes -- with one; S slices per chunk keep >= ~512 blocks in flight.
+__global__ __launch_bounds__(256) void gn_fused_kernel(const half_t* __restrict__ X, long ldx, int HW, int C, int G,
+                                                       int WC, int S, const half_t* __restrict__ gamma,
+                                                       const half_t* __restrict__ beta, float eps, int silu,
+                                                       half_t* __restrict__ Y, long ldy, float* __restrict__ scale,
+                                                       float* __restrict__ shift) {
+  __shared__ float red[256][17];
+  __shared__ float csum[2][256];
+  __shared__ float refs[32];
+  __shared__ float stat[32][2];
+  __shared__ float cscale[256], cshift[256];
+  const int nchunk = C / WC;
+  const int chunk = blockIdx.x % nchunk, slice = blockIdx.x / nchunk, img = blockIdx.y, tid = threadIdx.x;
+  const int cpg = C / G, c0 = chunk * WC, nq = WC / 8, R = 256 / nq, gc = WC / cpg;
+  const half_t* base = X + (long)img * HW * ldx + c0;
+  if (tid < gc) refs[tid] = (float)base[tid * cpg];
+  __syncthreads();
+  const int q = tid % nq, ph = tid / nq;
+  float rf[8], s1[8], s2[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { rf[i] = refs[min((q * 8 + i) / cpg, gc - 1)]; s1[i] = 0.f; s2[i] = 0.f; }
+  if (ph < R) {
+    const half_t* xp = base + (long)ph * ldx + q * 8;
+    const long step = (long)R * ldx;
+    int r = ph;
+    for (; r + 3 * R < HW; r += 4 * R, xp += 4 * step) {
+      const half8 v0 = *reinterpret_cast<const half8*>(xp);
+      const half8 v1 = *reinterpret_cast<const half8*>(xp + step);
+      const half8 v2 = *reinterpret_cast<const half8*>(xp + 2 * step);
+      const half8 v3 = *reinterpret_cast<const half8*>(xp + 3 * step);
+      gn_accum8(v0, rf, s1, s2);
+      gn_accum8(v1, rf, s1, s2);
+      gn_accum8(v2, rf, s1, s2);
+      gn_accum8(v3, rf, s1, s2);
+    }
+    for (; r < HW; r += R, xp += step) gn_accum8(*reinterpret_cast<const half8*>(xp), rf, s1, s2);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { red[tid][i] = s1[i]; red[tid][8 + i] = s2[i]; }
+  __syncthreads();
+  for (int c = tid; c < nq; c += 256) {
+    float a[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) a[i] = 0.f;
+    for (int p = 0; p < R; ++p)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) a[i] += red[p * nq + c][i];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { csum[0][c * 8 + i] = a[i]; csum[1][c * 8 + i] = a[8 + i]; }
+  }
+  __syncthreads();
+  if (tid < gc) {
+    double a = 0.0, b = 0.0;
+    for (int c = tid * cpg; c < (tid + 1) * cpg; ++c) { a += csum[0][c]; b += csum[1][c]; }
+    const double n = (double)HW * cpg;
+    const double m1 = a / n;
+    double var = b / n - m1 * m1;
+    if (var < 0) var = 0;
+    stat[tid][0] = (float)((double)refs[tid] + m1);
+    stat[tid][1] = (float)(1.0 / sqrt(var + (double)eps));
+  }
+  __syncthreads();
+  for (int c = tid; c < WC; c += 256) {
+    const int g = c / cpg, ch = c0 + c;
+    const float sc = stat[g][1] * (float)gamma[ch];
+    const float sh = (float)beta[ch] - stat[g][0] * sc;
+    cscale[c] = sc;
+    cshift[c] = sh;
+    if (slice == 0 && scale) {
+      scale[(long)img * C + ch] = sc;
+      shift[(long)img * C + ch] = sh;
+    }
+  }
+  __syncthreads();
+  // apply on rows [r0, r1) of this slice: the gn_apply_kernel arithmetic on the same fp32 scale / shift
+  const int r0 = (int)((long)HW * slice / S), r1 = (int)((long)HW * (slice + 1) / S);
+  float sc8[8], sh8[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sc8[j] = cscale[q * 8 + j]; sh8[j] = cshift[q * 8 + j]; }
+  if (ph >= R) return;
+  const long rowbase = (long)img * HW;
+  for (int r = r0 + ph; r < r1; r += R) {
+    const half8 x = *reinterpret_cast<const half8*>(X + (rowbase + r) * ldx + c0 + q * 8);
+    half8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float f = (float)x[j] * sc8[j] + sh8[j];
+      if (silu) f = silu_f(f);
+      o[j] = (half_t)f;
+    }
+    *reinterpret_cast<half8*>(Y + (rowbase + r) * ldy + c0 + q * 8) = o;
+  }
+}
+
 // One wave per (image, group): combine slices in fp64, emit scale = rstd*gamma, shift = beta - mean*scale.
 __global__ __launch_bounds__(64) void gn_finalize_kernel(const half_t* __restrict__ X, long ldx, int HW, int C,
                                                          int G, int S, const float2* __restrict__ part,
@@ -241,13 +355,8 @@ int groupnorm_impl(const void* X, long ldx, int nimg, int HW, int C, int groups,
   if (C % groups || C % 8 || ldx % 8 || C > 2560 || groups > 64) return SDMOE_ESHAPE;
   hipStream_t st = (hipStream_t)stream;
   if (HW <= GN_SMALL_HW) {
-    // chunk width: whole groups and whole 16-B chunks (lcm(cpg, 8)), doubled towards 80 channels while the chunk
-    // count stays integral
-    const int cpg = C / groups;
-    int wc = cpg;
-    while (wc % 8) wc += cpg;
-    while (wc < 80 && C % (2 * wc) == 0 && 2 * wc <= 256) wc *= 2;
-    if (wc <= 256 && wc / cpg <= 32 && C % wc == 0) {
+    const int wc = gn_chunk_width(C, groups);
+    if (wc) {
       gn_small_kernel<<<dim3(C / wc, nimg), 256, 0, st>>>((const half_t*)X, ldx, HW, C, groups, wc,
                                                           (const half_t*)gamma, (const half_t*)beta, eps, scale,
                                                           shift);
@@ -275,6 +384,12 @@ int groupnorm_impl(const void* X, long ldx, int nimg, int HW, int C, int groups,
 }
 }  // namespace
 
+int sdmoe_gn_set_fused(int v) {
+  if (v != 0 && v != 1) return SDMOE_EARG;
+  g_gn_fused = v;
+  return SDMOE_OK;
+}
+
 extern "C" int sdmoe_groupnorm_stats(const void* X, long ldx, int nimg, int HW, int C, int groups,
                                      const void* gamma, const void* beta, float eps, float* scale, float* shift,
                                      float* workspace, long workspace_floats, void* stream) {
@@ -286,8 +401,25 @@ extern "C" int sdmoe_groupnorm(const void* X, long ldx, int nimg, int HW, int C,
                                const void* beta, float eps, int silu, void* Y, long ldy, float* scale, float* shift,
                                float* workspace, long workspace_floats, void* stream) {
   if (!Y || ldy % 8) return Y ? SDMOE_ESHAPE : SDMOE_EARG;
-  // statistics then the wide-grid apply pass (folding the apply into gn_small_kernel's blocks measured 0.4-1 %
-  // slower end to end: 128-256 blocks stream the output far slower than the apply kernel's full grid)
+  // small latents: statistics + apply in one launch, the rows of each chunk split over S slices so the grid keeps
+  // >= ~512 blocks (one block per chunk -- 128-256 blocks -- streamed the output 0.4-1 % slower end to end)
+  if (g_gn_fused && HW <= GN_FUSED_HW && X && gamma && beta && nimg > 0 && groups > 0 && C % groups == 0 &&
+      C % 8 == 0 && ldx % 8 == 0 && groups <= 64) {
+    const int wc = gn_chunk_width(C, groups);
+    if (wc) {
+      const int nchunk = C / wc;
+      int S = (512 + nchunk * nimg - 1) / (nchunk * nimg);
+      const int R = 256 / (wc / 8);
+      if (S > HW / R) S = HW / R;  // every slice at least one row per row phase
+      if (S < 1) S = 1;
+      gn_fused_kernel<<<dim3(nchunk * S, nimg), 256, 0, (hipStream_t)stream>>>(
+          (const half_t*)X, ldx, HW, C, groups, wc, S, (const half_t*)gamma, (const half_t*)beta, eps, silu,
+          (half_t*)Y, ldy, scale, shift);
+      SDMOE_CHECK_LAUNCH();
+      return SDMOE_OK;
+    }
+  }
+  // statistics then the wide-grid apply pass
   int st = groupnorm_impl(X, ldx, nimg, HW, C, groups, gamma, beta, eps, scale, shift, workspace, workspace_floats,
                           stream);
   if (st != SDMOE_OK) return st;

@@ -317,7 +317,10 @@ int sdmoe_cfg_multistep_step(const void* eps, long lde, float* lat, int B, int H
    (0 auto, 1 = 128x160, 2 = 64x160, 3 = 256x320 8-wave, 4 = 256x160 8-wave, 5 = 256x320 4x2-wave, 6 = 128x320 8-wave); knob 2 = K-step
    depth (0 auto, 32, 64); knob 3 = MFMA-cluster wave priority (0/1); knob 4 = attention kernel (0 auto by shape,
    1 = 32x32x16 MFMA kernel, 2 / 4 = 16x16x32 kernel with 32 / 64 queries per wave, 64 for head_dim <= 40
-   only); knob 6 = GEMM diagnostics bits (1 no K-loop loads, 2 no MFMA, 4 no epilogue, 8 no global stores). */
+   only); knob 6 = GEMM diagnostics bits (1 no K-loop loads, 2 no MFMA, 4 no epilogue, 8 no global stores);
+   knob 7 = sdmoe_groupnorm at HW <= 256: 1 (default) statistics + apply in one launch, 0 two launches;
+   knob 8 = GEMM residual epilogue: 1 (default) output rounded to fp16 then the residual added in fp16 arithmetic
+   (diffusers' fp16 `linear(x) + residual`), 0 = accumulator + residual rounded once (fp32 staging). */
 int sdmoe_tune(int knob, int value);
 
 /* out = a + b (fp16, n % 8 == 0). */

@@ -475,6 +475,35 @@ def test_groupnorm_small_bench_shapes(H, C):
     close(y, F.silu(ref.permute(0, 2, 1).reshape(nimg * HW, C)), tol=5e-3)
 
 
+@pytest.mark.parametrize("HW,C,nimg,silu", [(1024, 640, 16, True), (1024, 320, 16, False), (1024, 1920, 16, True),
+                                            (256, 1280, 16, True), (256, 2560, 16, True), (256, 640, 5, False),
+                                            (64, 1280, 16, True), (64, 2560, 16, True), (64, 1280, 3, False),
+                                            (16, 128, 2, True), (1024, 960, 2, True)])
+def test_groupnorm_single_launch_bit_identical(HW, C, nimg, silu):
+    """gn_fused_kernel (statistics + apply in one launch, HW <= 1024) vs the two-launch path (gn_small_kernel +
+    gn_apply_kernel, sdmoe_tune knob 7 = 0): the same sums in the same order, the same fp64 finalize and the same
+    fp32 scale/shift, so output AND the returned scale/shift are bit-identical; strided input/output views."""
+    from sdmoe import _lib
+    lib = _lib.load()
+    buf = rnd(nimg * HW, C + 64, seed=HW + C) * 2 + 1
+    x = buf[:, 64:]
+    gamma, beta = rnd(C, scale=0.1, seed=C + 1) + 1, rnd(C, scale=0.1, seed=C + 2)
+    outs = []
+    for mode in (1, 0):
+        _lib.check(lib.sdmoe_tune(7, mode), "tune")
+        try:
+            dst = torch.full((nimg * HW, C + 16), 7.0, dtype=torch.float16, device=DEV)
+            ops.groupnorm(x, nimg, HW, gamma, beta, 1e-5, 32, silu, out=dst[:, 8:8 + C])
+            outs.append(dst)
+        finally:
+            _lib.check(lib.sdmoe_tune(7, 1), "tune")
+    assert torch.equal(outs[0], outs[1])
+    assert (outs[0][:, :8] == 7).all() and (outs[0][:, 8 + C:] == 7).all()
+    ref = F.group_norm(x.float().reshape(nimg, HW, C).permute(0, 2, 1), 32, gamma.float(), beta.float(), 1e-5)
+    ref = ref.permute(0, 2, 1).reshape(nimg * HW, C)
+    close(outs[0][:, 8:8 + C], F.silu(ref) if silu else ref, tol=5e-3)
+
+
 @pytest.mark.parametrize("H,C,Cin2,nimg", [(64, 320, 960, 2), (64, 320, 640, 3), (32, 640, 1920, 4), (32, 640, 320, 3),
                                            (16, 1280, 2560, 16), (16, 1280, 640, 5), (8, 1280, 2560, 16),
                                            (8, 1280, 1920, 3)])

@@ -1,0 +1,118 @@
+"""Per-launch device time of U-Net ops at the bench's shapes (16 images), under one or more sdmoe_tune settings.
+
+usage: python tools/micro_ab.py FAMILY [--tune "k=v,k=v"]... [--iters 50]
+FAMILY: gn | linear | conv | attn | all. Each case is launched back to back `iters` times between two HIP events on
+the launch stream (warm L2: a relative A/B tool, not the pipeline's cold-cache numbers: tools/op_breakdown.py)."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "diffusion-models-moe_amd"), ROOT]
+
+import torch  # noqa: E402
+
+from sdmoe import _lib, ops  # noqa: E402
+
+DEV = "cuda"
+N_IMG = 16
+
+
+def rnd(*shape, scale=1.0):
+    return (torch.randn(*shape, device=DEV) * scale).half()
+
+
+def gn_cases():
+    out = []
+    for HW, C in [(4096, 320), (4096, 640), (4096, 960), (1024, 640), (1024, 1280), (1024, 1920), (1024, 960),
+                  (256, 1280), (256, 2560), (256, 1920), (64, 1280), (64, 2560)]:
+        x = rnd(N_IMG * HW, C)
+        g, b = rnd(C) * 0.1 + 1, rnd(C) * 0.1
+        y = torch.empty_like(x)
+        out.append((f"groupnorm+silu HW={HW} C={C}", lambda x=x, g=g, b=b, y=y, HW=HW:
+                    ops.groupnorm(x, N_IMG, HW, g, b, 1e-5, 32, True, out=y), 3 * x.numel() * 2, "B"))
+    return out
+
+
+def linear_cases():
+    out = []
+    for M, N, K, res in [(65536, 320, 320, True), (65536, 320, 320, False), (16384, 640, 640, True),
+                         (16384, 640, 640, False), (4096, 1280, 1280, True), (4096, 1280, 1280, False),
+                         (65536, 960, 320, False), (1024, 1280, 1280, True)]:
+        x, w, bias = rnd(M, K), rnd(N, K, scale=K ** -0.5), rnd(N, scale=0.1)
+        r = rnd(M, N) if res else None
+        y = torch.empty(M, N, device=DEV, dtype=torch.float16)
+        out.append((f"linear M={M} N={N} K={K}{' +res' if res else ''}",
+                    lambda x=x, w=w, bias=bias, r=r, y=y: ops.linear(x, w, bias, residual=r, out=y), 2 * M * N * K, "F"))
+    return out
+
+
+def conv_cases():
+    out = []
+    for H, Cin, Cout in [(64, 320, 320), (32, 640, 640), (16, 1280, 1280), (8, 1280, 1280), (32, 1280, 640)]:
+        x = rnd(N_IMG * H * H, Cin)
+        w = ops.conv_weight(rnd(Cout, 3, 3, Cin, scale=(9 * Cin) ** -0.5))
+        out.append((f"conv {H}x{H} {Cin}->{Cout}", lambda x=x, w=w, H=H: ops.conv3x3(x, N_IMG, H, H, w),
+                    2 * N_IMG * H * H * Cout * 9 * Cin, "F"))
+    return out
+
+
+def attn_cases():
+    out = []
+    for N, C, heads in [(4096, 320, 8), (1024, 640, 8)]:
+        q = rnd(N_IMG * N, 3 * C)
+        d = C // heads
+        out.append((f"attn N={N} d={d}", lambda q=q, C=C, N=N, heads=heads:
+                    ops.attention(q[:, :C], q[:, C:2 * C], q[:, 2 * C:], N_IMG, N, N, heads),
+                    4 * N_IMG * heads * N * N * d, "F"))
+    return out
+
+
+def run(cases, iters):
+    res = {}
+    for name, f, work, unit in cases:
+        for _ in range(3):
+            f()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iters):
+            f()
+        e.record()
+        torch.cuda.synchronize()
+        us = s.elapsed_time(e) * 1e3 / iters
+        rate = work / (us * 1e-6) / (1e12 if unit == "F" else 1e9)
+        res[name] = (us, f"{rate:8.1f} {'TF/s' if unit == 'F' else 'GB/s'}")
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("family")
+    ap.add_argument("--tune", action="append", default=[])
+    ap.add_argument("--iters", type=int, default=50)
+    a = ap.parse_args()
+    lib = _lib.load()
+    fam = {"gn": gn_cases, "linear": linear_cases, "conv": conv_cases, "attn": attn_cases}
+    cases = [c for k in (fam if a.family == "all" else [a.family]) for c in fam[k]()]
+    settings = a.tune or [""]
+    table = {}
+    for rep in range(2):  # interleaved twice
+        for st in settings:
+            for kv in filter(None, st.split(",")):
+                k, v = kv.split("=")
+                _lib.check(lib.sdmoe_tune(int(k), int(v)), "tune")
+            r = run(cases, a.iters)
+            for kv in filter(None, st.split(",")):  # back to defaults (0) unless the knob's default differs
+                k, _ = kv.split("=")
+                _lib.check(lib.sdmoe_tune(int(k), 1 if k == "7" else 0), "tune")
+            for name, v in r.items():
+                table.setdefault(name, {}).setdefault(st, []).append(v)
+    for name, per in table.items():
+        cols = "  ".join(f"[{st or 'default'}] " + " / ".join(f"{us:7.2f} us" for us, _ in v) + f" {v[-1][1]}"
+                         for st, v in per.items())
+        print(f"{name:36s} {cols}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
