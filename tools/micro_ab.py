@@ -59,12 +59,19 @@ def conv_cases():
 
 def attn_cases():
     out = []
-    for N, C, heads in [(4096, 320, 8), (1024, 640, 8)]:
+    for N, C, heads in [(4096, 320, 8), (1024, 640, 8), (256, 1280, 8), (64, 1280, 8)]:
         q = rnd(N_IMG * N, 3 * C)
         d = C // heads
         out.append((f"attn N={N} d={d}", lambda q=q, C=C, N=N, heads=heads:
                     ops.attention(q[:, :C], q[:, C:2 * C], q[:, 2 * C:], N_IMG, N, N, heads),
                     4 * N_IMG * heads * N * N * d, "F"))
+    for N, C, heads in [(4096, 320, 8), (1024, 640, 8), (256, 1280, 8)]:  # cross-attention, 77 text keys
+        q = rnd(N_IMG * N, C)
+        kv = rnd(N_IMG * 77, 2 * C)
+        d = C // heads
+        out.append((f"attn N={N} Nk=77 d={d}", lambda q=q, kv=kv, C=C, N=N, heads=heads:
+                    ops.attention(q, kv[:, :C], kv[:, C:], N_IMG, N, 77, heads),
+                    4 * N_IMG * heads * N * 77 * d, "F"))
     return out
 
 
@@ -105,7 +112,7 @@ def main():
             r = run(cases, a.iters)
             for kv in filter(None, st.split(",")):  # back to defaults (0) unless the knob's default differs
                 k, _ = kv.split("=")
-                _lib.check(lib.sdmoe_tune(int(k), 1 if k == "7" else 0), "tune")
+                _lib.check(lib.sdmoe_tune(int(k), 1 if k in ("7", "8") else 0), "tune")
             for name, v in r.items():
                 table.setdefault(name, {}).setdefault(st, []).append(v)
     for name, per in table.items():
