@@ -9,7 +9,7 @@ cd /tmp && export TMPDIR=/tmp
 for spec in "conv 0" "conv 4" "geglu 0" "attn 0"; do
   set -- $spec
   what=$1; dg=$2; i=0
-  for c in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE" "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MFMA SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES" "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT"; do
+  for c in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE" "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MFMA SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES" "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT" "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS"; do
     i=$((i+1))
     timeout -s KILL 90 rocprofv3 --pmc $c -d $R/gpurun_out/pmu_${what}${dg}_$i -o run --output-format csv -- python3 $R/tools/kernel_micro.py $what --iters 5 --diag $dg > $R/gpurun_out/pmu_${what}${dg}_$i.log 2>&1
   done
