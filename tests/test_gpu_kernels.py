@@ -524,3 +524,4 @@ def test_conv3x3_folded_shortcut(H, C, Cin2, nimg):
     ref = F.conv2d(xi, w.float(), b.float(), padding=1).permute(0, 2, 3, 1).reshape(-1, C)
     ref = ref + x.float() @ wsc.float().t() + cadd.float().repeat_interleave(H * H, 0)
     close(out, ref)
+

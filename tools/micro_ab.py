@@ -1,7 +1,7 @@
 """Per-launch device time of U-Net ops at the bench's shapes (16 images), under one or more sdmoe_tune settings.
 
 usage: python tools/micro_ab.py FAMILY [--tune "k=v,k=v"]... [--iters 50]
-FAMILY: gn | linear | conv | attn | all. Each case is launched back to back `iters` times between two HIP events on
+FAMILY: gn | linear | geglu | conv | attn | all. Each case is launched back to back `iters` times between two HIP events on
 the launch stream (warm L2: a relative A/B tool, not the pipeline's cold-cache numbers: tools/op_breakdown.py)."""
 import argparse
 import os
@@ -44,6 +44,25 @@ def linear_cases():
         y = torch.empty(M, N, device=DEV, dtype=torch.float16)
         out.append((f"linear M={M} N={N} K={K}{' +res' if res else ''}",
                     lambda x=x, w=w, bias=bias, r=r, y=y: ops.linear(x, w, bias, residual=r, out=y), 2 * M * N * K, "F"))
+    return out
+
+
+def geglu_cases():
+    """The fused routed GEGLU projection (relu, expert 20, top-k 0.2) and the LN-folded QKV at each U-Net level."""
+    out = []
+    for M, C in [(65536, 320), (16384, 640), (4096, 1280)]:
+        F, E = 4 * C, 4 * C // 20
+        x = rnd(M, C)
+        w = rnd(2 * F, C, scale=C ** -0.5)
+        routing = ops.Routing(torch.randperm(F) % E, E, E // 5, DEV)
+        w_il, b_il = ops.interleave_geglu(w, rnd(2 * F, scale=0.1), routing.perm)
+        score = torch.empty(M, E, device=DEV, dtype=torch.float16)
+        o = torch.empty(M, F, device=DEV, dtype=torch.float16)
+        out.append((f"geglu M={M} N={2 * F} K={C}", lambda x=x, w_il=w_il, b_il=b_il, score=score, o=o, r=routing:
+                    ops.linear_geglu(x, w_il, b_il, ops.ACT_RELU, score=score, esize=r.esize, out=o),
+                    2 * M * 2 * F * C, "F"))
+        fold = ops.LNFold(rnd(3 * C, C, scale=C ** -0.5), rnd(C) * 0.1 + 1, rnd(C) * 0.1, 1e-5)
+        out.append((f"linear_ln M={M} N={3 * C} K={C}", lambda x=x, f=fold: ops.linear_ln(x, f), 2 * M * 3 * C * C, "F"))
     return out
 
 
@@ -100,7 +119,7 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     a = ap.parse_args()
     lib = _lib.load()
-    fam = {"gn": gn_cases, "linear": linear_cases, "conv": conv_cases, "attn": attn_cases}
+    fam = {"gn": gn_cases, "linear": linear_cases, "geglu": geglu_cases, "conv": conv_cases, "attn": attn_cases}
     cases = [c for k in (fam if a.family == "all" else [a.family]) for c in fam[k]()]
     settings = a.tune or [""]
     table = {}
