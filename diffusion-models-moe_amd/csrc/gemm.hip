@@ -37,6 +37,7 @@ int g_tile = 0;
 int g_bk = 0;
 int g_prio = 0;
 int g_res16 = 1;  // knob 8: 1 = residual epilogues on the fp16 staging path (residual added in the copy-out), 0 = fp32
+int g_ksplit = 0;  // knob 9: forced split-K factor (0 = auto; 1 = never split), for tile sweeps
 int g_diag = 0;  // knob 6, diagnostics only (results garbage): bit 0 = no K-loop operand loads, bit 1 = no MFMAs,
                  // bit 2 = no epilogue (nothing stored), bit 3 = epilogue without its global stores
 
@@ -83,6 +84,10 @@ struct GemmParams {
   // (the block input at the output pixel, row stride lda2) against the shortcut weights appended to W's rows
   const half_t* A2; long lda2;
   int a2_bytes;
+  // GroupNorm folded into the GEMM (sdmoe_linear_per_image): image i = m / rows_per_batch multiplies its own weights
+  // W + i * w_bstride (0 = one weight set) and adds colf[i * colf_bstride + n] (fp32 per-image column add)
+  long w_bstride;
+  const float* colf; long colf_bstride;
 };
 
 SDMOE_DEV int swz(int row) { return (row >> 1) & 7; }
@@ -106,6 +111,12 @@ SDMOE_DEV void epilogue8(const GemmParams& p, int m, int n, float (&v)[8]) {
     half8 cc = *reinterpret_cast<const half8*>(p.coladd + (long)b * p.coladd_bstride + n);
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] += (float)cc[j];
+  }
+  if (p.colf) {
+    const float* cf = p.colf + (long)(m / p.rows_per_batch) * p.colf_bstride + n;
+    const float4v c0 = *reinterpret_cast<const float4v*>(cf), c1 = *reinterpret_cast<const float4v*>(cf + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] += c0[j]; v[4 + j] += c1[j]; }
   }
   if (p.act != ACT_NONE) {
 #pragma unroll
@@ -172,7 +183,8 @@ SDMOE_DEV void expert_sums(const GemmParams& p, const half_t* sg, int mrow0, int
 }
 
 template <int BM, int BN, int WMW, int WNW, int MODE, int NSTAGE, int BKT>
-__global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 : 1)) void gemm_kernel(GemmParams p) {
+__global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || BM * BN <= 20480) ? 2 : 1)) void gemm_kernel(
+    GemmParams p) {
   constexpr int BK = BKT;                        // K per stage: 64 (128-B rows) or 32 (64-B rows, deeper ring)
   constexpr int RB = BK * 2, CPRW = BK / 8;      // LDS row bytes, 16-B chunks per row
   constexpr int RPP = 1024 / RB;                 // rows per 1-KiB LDS-DMA piece
@@ -242,7 +254,9 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
   // ---- LDS-DMA sources: buffer loads through two SRDs (A, W); an out-of-range offset (OOB) is dropped by the
   // hardware range check and lands as zeros, which gives conv halo rows and M/N tails for free.
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.a_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsW = __builtin_amdgcn_make_buffer_rsrc((void*)p.W, (short)0, p.w_bytes, 0x00020000);
+  // per-image weights (sdmoe_linear_per_image): a tile never straddles two images (host check rows_per_batch % BM)
+  const half_t* Wimg = p.w_bstride ? p.W + (long)(m0 / p.rows_per_batch) * p.w_bstride : p.W;
+  const __amdgpu_buffer_rsrc_t rsW = __builtin_amdgcn_make_buffer_rsrc((void*)Wimg, (short)0, p.w_bytes, 0x00020000);
   const int lrow = lane / CPRW, lch = lane % CPRW;
   // A rows: wave w stages rows [8*(w*A_PW + j), +8); B rows likewise with B_PW
   unsigned avoff[A_PW];  // GEMM: byte offset of (row, pre-swizzled chunk); conv: of the centre-tap pixel
@@ -593,6 +607,7 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
         __builtin_amdgcn_sched_barrier(0);
         const int m = mw + 16 * (h * (FM / NPASS16) + i) + fr;
         const half_t* cap = (p.coladd && m < p.M) ? p.coladd + (long)(m / p.rows_per_batch) * p.coladd_bstride : nullptr;
+        const float* cfp = (p.colf && m < p.M) ? p.colf + (long)(m / p.rows_per_batch) * p.colf_bstride : nullptr;
         float a = 0.f, c = 0.f;  // LN: this lane's row (rstd, -mean * rstd), read once per fragment row
         if constexpr (LN) {
           const int rl = wr * WM + 16 * (h * (FM / NPASS16) + i) + fr;
@@ -616,6 +631,11 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && WMW * WNW == 4 ? 2 
             const half4 c = *reinterpret_cast<const half4*>(cap + n);
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] += (float)c[r];
+          }
+          if (cfp && n < p.N) {
+            const float4v c = *reinterpret_cast<const float4v*>(cfp + n);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += c[r];
           }
           half4 y;
 #pragma unroll
@@ -790,9 +810,14 @@ template <int BM, int BN, int WMW, int WNW, int MODE>
 int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
   const int ntiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
   const int nk = p.K / 64;
+  if (p.w_bstride && p.rows_per_batch % BM) return SDMOE_EUNSUP;  // a tile would straddle two images' weights
   int ksplit = 1;
   // fill the chip: split K when the tile grid covers well under one wave of 256 CUs
-  if (ws && ntiles < 192 && nk >= 16) {
+  if (ws && g_ksplit > 0) {
+    ksplit = g_ksplit;
+    if (ksplit > nk) ksplit = nk;
+    while (ksplit > 1 && (long)ksplit * p.M * p.N > ws_floats) --ksplit;
+  } else if (ws && ntiles < 192 && nk >= 16) {
     ksplit = (256 + ntiles - 1) / ntiles;
     if (ksplit > 8) ksplit = 8;
     if (ksplit > nk / 4) ksplit = nk / 4;
@@ -840,6 +865,7 @@ int dispatch_geglu(const GemmParams& p, hipStream_t s) {
   const int nt160_128 = ((p.M + 127) / 128) * (p.N / 160);
   if (g_tile == 1) return launch_tile<128, 160, 2, 2, MODE>(p, nullptr, 0, s);
   if (g_tile == 4) return launch_tile<256, 160, 4, 2, MODE>(p, nullptr, 0, s);
+  if (g_tile == 7) return launch_tile<128, 160, 4, 2, MODE>(p, nullptr, 0, s);  // sweep: two workgroups per CU
   if (p.N % 320 == 0 && nt320 >= 240) {
     // 2x4 waves (wave tile 128 rows x 40 neurons): with the row-fastest epilogue its 32-row staging passes are
     // conflict-free (4x2's 16-row passes are not: two 16-lane b128 groups mix column pairs); 174.6 vs 181.2 us at
@@ -861,6 +887,11 @@ int dispatch(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
   if (g_tile == 4 && p.N % 160 == 0) return launch_tile<256, 160, 4, 2, MODE>(p, ws, ws_floats, s);
   if (g_tile == 5 && p.N % 320 == 0) return launch_tile<256, 320, 4, 2, MODE>(p, ws, ws_floats, s);
   if (g_tile == 6 && p.N % 320 == 0) return launch_tile<128, 320, 2, 4, MODE>(p, ws, ws_floats, s);
+  // sweep-only 8-wave tiles with a 32x80 wave tile (two workgroups per CU on a 2-stage ring)
+  if constexpr (MODE == MODE_GEMM || MODE == MODE_CONV || MODE == MODE_GEMM_LN) {
+    if (g_tile == 7 && p.N % 160 == 0) return launch_tile<128, 160, 4, 2, MODE>(p, ws, ws_floats, s);
+    if (g_tile == 8 && p.N % 320 == 0) return launch_tile<64, 320, 2, 4, MODE>(p, ws, ws_floats, s);
+  }
   // 8-wave 256x320 tile (wave tile 128x80: 2.5x the MFMA work per LDS byte of 64x80) whenever it alone fills
   // the chip; 256x160 8-wave + split-K for long-K problems whose 128x160 grid is under ~1.2 waves of CUs.
   // Measured on MI355X with tools/gemm_bench.py --tile.
@@ -1008,6 +1039,38 @@ __global__ __launch_bounds__(256) void ln_fold_kernel(const half_t* __restrict__
   }
 }
 
+// GroupNorm fold (sdmoe_gn_fold): one wave per (image, output row n): Wf[i][n, k] = fp16(W[n, k] * scale[i, k]) and
+// colbias[i][n] = bias[n] + sum_k W[n, k] * shift[i, k] (fp32, fixed-order lane sums + xor tree: deterministic)
+__global__ __launch_bounds__(256) void gn_fold_kernel(const half_t* __restrict__ W, long ldw, int N, int K,
+                                                      const half_t* __restrict__ bias, const float* __restrict__ scale,
+                                                      const float* __restrict__ shift, half_t* __restrict__ Wf,
+                                                      float* __restrict__ colbias) {
+  const int lane = threadIdx.x & 63;
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6), img = blockIdx.y;
+  if (n >= N) return;
+  const float* sc = scale + (long)img * K;
+  const float* sh = shift + (long)img * K;
+  half_t* wo = Wf + ((long)img * N + n) * K;
+  float acc = 0.f;
+  for (int k = lane * 8; k < K; k += 512) {
+    const half8 w = *reinterpret_cast<const half8*>(W + (long)n * ldw + k);
+    const float4v s0 = *reinterpret_cast<const float4v*>(sc + k), s1 = *reinterpret_cast<const float4v*>(sc + k + 4);
+    const float4v h0 = *reinterpret_cast<const float4v*>(sh + k), h1 = *reinterpret_cast<const float4v*>(sh + k + 4);
+    const float s[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+    const float h[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+    half8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      o[j] = (half_t)((float)w[j] * s[j]);
+      acc = __builtin_fmaf((float)w[j], h[j], acc);
+    }
+    *reinterpret_cast<half8*>(wo + k) = o;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (lane == 0) colbias[(long)img * N + n] = acc + (bias ? (float)bias[n] : 0.f);
+}
+
 int grid_for(long n) {
   long g = (n + 255) / 256;
   return (int)(g > 4096 ? 4096 : (g < 1 ? 1 : g));
@@ -1031,6 +1094,37 @@ extern "C" int sdmoe_linear(const void* A, long lda, const void* W, long ldw, co
   p.rows_per_batch = rows_per_batch > 0 ? rows_per_batch : 1;
   const long ab = ((long)(M - 1) * lda + K) * 2, wb = ((long)(N - 1) * ldw + K) * 2;
   if (ab >= (long)OOB || wb >= (long)OOB) return SDMOE_ESHAPE;
+  p.a_bytes = (int)ab; p.w_bytes = (int)wb;
+  return dispatch<MODE_GEMM>(p, workspace, workspace_floats, (hipStream_t)stream);
+}
+
+extern "C" int sdmoe_gn_fold(const void* W, long ldw, int N, int K, const void* bias, const float* scale,
+                             const float* shift, int nimg, void* Wf, float* colbias, void* stream) {
+  if (N == 0 || nimg == 0) return SDMOE_OK;
+  if (!W || !scale || !shift || !Wf || !colbias || N < 0 || K <= 0 || nimg < 0) return SDMOE_EARG;
+  if (K % 8 || ldw % 8 || ldw < K) return SDMOE_ESHAPE;
+  gn_fold_kernel<<<dim3((N + 3) / 4, nimg), 256, 0, (hipStream_t)stream>>>(
+      (const half_t*)W, ldw, N, K, (const half_t*)bias, scale, shift, (half_t*)Wf, colbias);
+  SDMOE_CHECK_LAUNCH();
+  return SDMOE_OK;
+}
+
+extern "C" int sdmoe_linear_per_image(const void* A, long lda, const void* Wf, long ldw, long w_bstride,
+                                      const float* colbias, long colbias_bstride, int rows_per_batch, const void* R,
+                                      long ldr, void* C, long ldc, int M, int N, int K, float* workspace,
+                                      long workspace_floats, void* stream) {
+  if (M == 0) return SDMOE_OK;
+  if (!A || !Wf || !C || M < 0 || N <= 0 || K <= 0 || rows_per_batch <= 0 || w_bstride <= 0) return SDMOE_EARG;
+  if (K % 64 || N % 8 || lda % 8 || ldw % 8 || ldc % 8 || (R && ldr % 8) || rows_per_batch % 256 ||
+      M % rows_per_batch || w_bstride % 8 || (colbias && colbias_bstride % 4))
+    return SDMOE_ESHAPE;
+  GemmParams p{};
+  p.A = (const half_t*)A; p.lda = lda; p.W = (const half_t*)Wf; p.ldw = ldw; p.w_bstride = w_bstride;
+  p.colf = colbias; p.colf_bstride = colbias_bstride;
+  p.R = (const half_t*)R; p.ldr = ldr; p.C = (half_t*)C; p.ldc = ldc;
+  p.M = M; p.N = N; p.K = K; p.act = ACT_NONE; p.rows_per_batch = rows_per_batch;
+  const long ab = ((long)(M - 1) * lda + K) * 2, wb = ((long)(N - 1) * ldw + K) * 2;
+  if (ab >= (long)OOB || wb >= (long)OOB || (long)(M / rows_per_batch) * w_bstride * 2 >= (long)OOB) return SDMOE_ESHAPE;
   p.a_bytes = (int)ab; p.w_bytes = (int)wb;
   return dispatch<MODE_GEMM>(p, workspace, workspace_floats, (hipStream_t)stream);
 }
@@ -1217,7 +1311,8 @@ extern "C" int sdmoe_tune(int knob, int value) {
   if (knob == 4) return sdmoe_attn_set_nqf(value);
   if (knob == 7) return sdmoe_gn_set_fused(value);
   if (knob == 0 && (value == 0 || value == 2 || value == 3)) { g_stages = value; return SDMOE_OK; }
-  if (knob == 1 && value >= 0 && value <= 6) { g_tile = value; return SDMOE_OK; }
+  if (knob == 1 && value >= 0 && value <= 8) { g_tile = value; return SDMOE_OK; }
+  if (knob == 9 && value >= 0 && value <= 16) { g_ksplit = value; return SDMOE_OK; }
   if (knob == 2 && (value == 0 || value == 32 || value == 64)) { g_bk = value; return SDMOE_OK; }
   if (knob == 3 && (value == 0 || value == 1)) { g_prio = value; return SDMOE_OK; }
   if (knob == 6 && value >= 0 && value <= 15) { g_diag = value; return SDMOE_OK; }

@@ -12,7 +12,8 @@
 namespace {
 
 constexpr int GN_SMALL_HW = 1024;  // latents up to 32x32 take the single-launch path (measured crossover)
-int g_gn_fused = 1;  // sdmoe_tune knob 7: 1 = gn_fused_kernel for HW <= GN_FUSED_HW (sdmoe_groupnorm), 0 = two launches
+int g_gn_fused = 1;  // sdmoe_tune knob 7, sdmoe_groupnorm at HW <= GN_FUSED_HW: 1 = gn_fused_reg_kernel (rows held in
+                     // registers), 2 = gn_fused_kernel (rows re-read for the apply), 0 = two launches
 // single-launch statistics + apply up to 16x16 latents: 13.0 vs 15.9 us at 8x8 (C = 1280, 16 images), 14.5 vs 16.0
 // at 16x16; at 32x32 it is slower (21.9 vs 21.1 us, C = 640; 47.6 vs 42.2 at C = 1920): every block re-reads its
 // chunk's 1024 rows with 16 KB in flight, which no longer hides behind the saved launch (tools/micro_ab.py gn)
@@ -270,6 +271,99 @@ __global__ __launch_bounds__(256) void gn_fused_kernel(const half_t* __restrict_
   }
 }
 
+// gn_fused_kernel with its latency chain cut (sdmoe_tune knob 7 = 1, default; 2 = the kernel above): every row of
+// the thread's chunk (RMAX at most) is loaded into registers up front -- before the barrier that publishes the
+// group references -- together with its gamma / beta, so the kernel waits on global memory once; the row-phase
+// reduction runs on nq x 16 threads instead of nq; the apply reads the rows from those registers (no second global
+// read) and each block stores the rows of its slice [r0, r1). Same sums in the same order as gn_small_kernel +
+// gn_apply_kernel: bit-identical output, scale and shift.
+template <int RMAX>
+__global__ __launch_bounds__(256) void gn_fused_reg_kernel(const half_t* __restrict__ X, long ldx, int HW, int C,
+                                                           int G, int WC, int S, const half_t* __restrict__ gamma,
+                                                           const half_t* __restrict__ beta, float eps, int silu,
+                                                           half_t* __restrict__ Y, long ldy, float* __restrict__ scale,
+                                                           float* __restrict__ shift) {
+  __shared__ float red[256][17];
+  __shared__ float csum[2][256];
+  __shared__ float refs[32];
+  __shared__ float stat[32][2];
+  const int nchunk = C / WC;
+  const int chunk = blockIdx.x % nchunk, slice = blockIdx.x / nchunk, img = blockIdx.y, tid = threadIdx.x;
+  const int cpg = C / G, c0 = chunk * WC, nq = WC / 8, R = 256 / nq, gc = WC / cpg;
+  const half_t* base = X + (long)img * HW * ldx + c0;
+  const int q = tid % nq, ph = tid / nq;
+  const bool live = ph < R;
+  half8 v[RMAX];
+#pragma unroll
+  for (int k = 0; k < RMAX; ++k) {
+    const int r = ph + k * R;
+    v[k] = (live && r < HW) ? *reinterpret_cast<const half8*>(base + (long)r * ldx + q * 8)
+                            : (half8){0, 0, 0, 0, 0, 0, 0, 0};
+  }
+  const half8 gm8 = *reinterpret_cast<const half8*>(gamma + c0 + q * 8);
+  const half8 bt8 = *reinterpret_cast<const half8*>(beta + c0 + q * 8);
+  if (tid < gc) refs[tid] = (float)base[tid * cpg];
+  __syncthreads();
+  float rf[8], s1[8], s2[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { rf[i] = refs[min((q * 8 + i) / cpg, gc - 1)]; s1[i] = 0.f; s2[i] = 0.f; }
+#pragma unroll
+  for (int k = 0; k < RMAX; ++k)
+    if (live && ph + k * R < HW) gn_accum8(v[k], rf, s1, s2);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { red[tid][i] = s1[i]; red[tid][8 + i] = s2[i]; }
+  __syncthreads();
+  if (tid < nq * 16) {  // (chunk c, value i): the R row phases in order, as gn_small_kernel's per-c loop
+    const int c = tid >> 4, i = tid & 15;
+    float a = 0.f;
+    for (int p = 0; p < R; ++p) a += red[p * nq + c][i];
+    csum[i >> 3][c * 8 + (i & 7)] = a;
+  }
+  __syncthreads();
+  if (tid < gc) {
+    double a = 0.0, b = 0.0;
+    for (int c = tid * cpg; c < (tid + 1) * cpg; ++c) { a += csum[0][c]; b += csum[1][c]; }
+    const double n = (double)HW * cpg;
+    const double m1 = a / n;
+    double var = b / n - m1 * m1;
+    if (var < 0) var = 0;
+    stat[tid][0] = (float)((double)refs[tid] + m1);
+    stat[tid][1] = (float)(1.0 / sqrt(var + (double)eps));
+  }
+  __syncthreads();
+  if (slice == 0 && scale) {
+    for (int c = tid; c < WC; c += 256) {
+      const int g = c / cpg, ch = c0 + c;
+      const float sc = stat[g][1] * (float)gamma[ch];
+      scale[(long)img * C + ch] = sc;
+      shift[(long)img * C + ch] = (float)beta[ch] - stat[g][0] * sc;
+    }
+  }
+  if (!live) return;
+  float sc8[8], sh8[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int g = min((q * 8 + j) / cpg, gc - 1);
+    sc8[j] = stat[g][1] * (float)gm8[j];
+    sh8[j] = (float)bt8[j] - stat[g][0] * sc8[j];
+  }
+  const int r0 = (int)((long)HW * slice / S), r1 = (int)((long)HW * (slice + 1) / S);
+  const long rowbase = (long)img * HW;
+#pragma unroll
+  for (int k = 0; k < RMAX; ++k) {
+    const int r = ph + k * R;
+    if (r < r0 || r >= r1) continue;
+    half8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float f = (float)v[k][j] * sc8[j] + sh8[j];
+      if (silu) f = silu_f(f);
+      o[j] = (half_t)f;
+    }
+    *reinterpret_cast<half8*>(Y + (rowbase + r) * ldy + c0 + q * 8) = o;
+  }
+}
+
 // One wave per (image, group): combine slices in fp64, emit scale = rstd*gamma, shift = beta - mean*scale.
 __global__ __launch_bounds__(64) void gn_finalize_kernel(const half_t* __restrict__ X, long ldx, int HW, int C,
                                                          int G, int S, const float2* __restrict__ part,
@@ -385,7 +479,7 @@ int groupnorm_impl(const void* X, long ldx, int nimg, int HW, int C, int groups,
 }  // namespace
 
 int sdmoe_gn_set_fused(int v) {
-  if (v != 0 && v != 1) return SDMOE_EARG;
+  if (v < 0 || v > 2) return SDMOE_EARG;
   g_gn_fused = v;
   return SDMOE_OK;
 }
@@ -412,9 +506,18 @@ extern "C" int sdmoe_groupnorm(const void* X, long ldx, int nimg, int HW, int C,
       const int R = 256 / (wc / 8);
       if (S > HW / R) S = HW / R;  // every slice at least one row per row phase
       if (S < 1) S = 1;
-      gn_fused_kernel<<<dim3(nchunk * S, nimg), 256, 0, (hipStream_t)stream>>>(
-          (const half_t*)X, ldx, HW, C, groups, wc, S, (const half_t*)gamma, (const half_t*)beta, eps, silu,
-          (half_t*)Y, ldy, scale, shift);
+      const dim3 grid(nchunk * S, nimg);
+      hipStream_t st = (hipStream_t)stream;
+      const half_t *x = (const half_t*)X, *g = (const half_t*)gamma, *b = (const half_t*)beta;
+      const int rpt = (HW + R - 1) / R;  // rows per thread of the register-resident kernel
+      if (g_gn_fused == 1 && rpt <= 16) {
+        if (rpt <= 4) gn_fused_reg_kernel<4><<<grid, 256, 0, st>>>(x, ldx, HW, C, groups, wc, S, g, b, eps, silu, (half_t*)Y, ldy, scale, shift);
+        else if (rpt <= 8) gn_fused_reg_kernel<8><<<grid, 256, 0, st>>>(x, ldx, HW, C, groups, wc, S, g, b, eps, silu, (half_t*)Y, ldy, scale, shift);
+        else gn_fused_reg_kernel<16><<<grid, 256, 0, st>>>(x, ldx, HW, C, groups, wc, S, g, b, eps, silu, (half_t*)Y, ldy, scale, shift);
+      } else {
+        gn_fused_kernel<<<grid, 256, 0, st>>>(x, ldx, HW, C, groups, wc, S, g, b, eps, silu, (half_t*)Y, ldy, scale,
+                                              shift);
+      }
       SDMOE_CHECK_LAUNCH();
       return SDMOE_OK;
     }

@@ -26,6 +26,8 @@ SIGNATURES = {
     "sdmoe_mask_weight": [_P, _P, _L, _L, _P, _P],
     "sdmoe_groupnorm_stats": [_P, _L, _I, _I, _I, _I, _P, _P, _F, _P, _P, _P, _L, _P],
     "sdmoe_groupnorm": [_P, _L, _I, _I, _I, _I, _P, _P, _F, _I, _P, _L, _P, _P, _P, _L, _P],
+    "sdmoe_gn_fold": [_P, _L, _I, _I, _P, _P, _P, _I, _P, _P, _P],
+    "sdmoe_linear_per_image": [_P, _L, _P, _L, _L, _P, _L, _I, _P, _L, _P, _L, _I, _I, _I, _P, _L, _P],
     "sdmoe_layernorm": [_P, _L, _P, _L, _I, _I, _P, _P, _F, _P],
     "sdmoe_ln_fold": [_P, _L, _I, _I, _P, _P, _P, _P, _L, _P, _P, _P],
     "sdmoe_linear_ln": [_P, _L, _P, _L, _P, _P, _F, _P, _L, _I, _I, _I, _P],

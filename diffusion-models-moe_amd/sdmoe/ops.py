@@ -292,6 +292,45 @@ def groupnorm(x, nimg, HW, gamma, beta, eps, groups=32, silu=False, out=None):
     return out
 
 
+def gn_fold(w, bias, scale, shift):
+    """Per-image GroupNorm-folded weights of a linear (sdmoe_gn_fold): Wf [nimg, N, K] fp16 and colbias [nimg, N]
+    fp32 with x . Wf[i]^T + colbias[i] = GN(x) . w^T + bias on the rows of image i (scale / shift from
+    groupnorm_stats)."""
+    lib = _lib.load()
+    N, K = w.shape
+    nimg = scale.shape[0]
+    if tuple(scale.shape) != (nimg, K) or tuple(shift.shape) != (nimg, K):
+        raise ValueError(f"gn_fold: scale/shift {tuple(scale.shape)} do not match weight {tuple(w.shape)}")
+    wf = torch.empty((nimg, N, K), dtype=torch.float16, device=w.device)
+    cb = torch.empty((nimg, N), dtype=torch.float32, device=w.device)
+    st = lib.sdmoe_gn_fold(_dev(w, "w"), w.stride(0), N, K, _ptr(bias), _dev(scale, "scale", torch.float32),
+                           _dev(shift, "shift", torch.float32), nimg, wf.data_ptr(), cb.data_ptr(), _stream())
+    _lib.check(st, "sdmoe_gn_fold")
+    return wf, cb
+
+
+def linear_per_image(x, wf, colbias, rows_per_batch, *, residual=None, out=None):
+    """out[m] = x[m] . wf[m // rows_per_batch]^T + colbias[m // rows_per_batch] (+ residual): the GEMM behind a folded
+    GroupNorm (sdmoe_linear_per_image; rows_per_batch % 256 == 0)."""
+    lib = _lib.load()
+    xp, lda = _rows(x, "x")
+    M, K = x.shape
+    nimg, N, Kw = wf.shape
+    if Kw != K or M != nimg * rows_per_batch or tuple(colbias.shape) != (nimg, N):
+        raise ValueError(f"linear_per_image: x {tuple(x.shape)}, wf {tuple(wf.shape)}, colbias "
+                         f"{tuple(colbias.shape)}, rows_per_batch {rows_per_batch}")
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float16, device=x.device)
+    op, ldc = _rows(out, "out")
+    rp, ldr = (None, 0) if residual is None else _rows(residual, "residual")
+    ws = _workspace(x.device)
+    st = lib.sdmoe_linear_per_image(xp, lda, _dev(wf, "wf"), wf.stride(1), wf.stride(0),
+                                    _dev(colbias, "colbias", torch.float32), colbias.stride(0), rows_per_batch, rp,
+                                    ldr, op, ldc, M, N, K, ws.data_ptr(), ws.numel(), _stream())
+    _lib.check(st, "sdmoe_linear_per_image")
+    return out
+
+
 def layernorm(x, gamma, beta, eps=1e-5, out=None):
     lib = _lib.load()
     xp, ldx = _rows(x, "x")

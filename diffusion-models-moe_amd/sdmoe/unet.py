@@ -34,6 +34,10 @@ FUSED_LN = os.environ.get("SDMOE_FUSED_LN", "1") != "0"
 FUSED_LN_FFN = os.environ.get("SDMOE_FUSED_LN_FFN", "0") == "1"  # norm3 into the GEGLU GEMM too (slower, see run)
 # ResnetBlock2D conv_shortcut (1x1) folded into conv2 as extra K-steps (sdmoe_conv3x3_sc; SDMOE_FUSED_SC=0: separate)
 FUSED_SC = os.environ.get("SDMOE_FUSED_SC", "1") != "0"
+# Transformer2DModel GroupNorm folded into proj_in (per-image weights, sdmoe_gn_fold + sdmoe_linear_per_image) at
+# latents of >= 32x32 (SDMOE_FUSED_GN=0: GroupNorm apply pass + proj_in, A/B)
+FUSED_GN = os.environ.get("SDMOE_FUSED_GN", "1") != "0"
+GN_FOLD_MIN_HW = 1024
 IN_PAD = 64    # conv_in input channels padded 4 -> 64 (K-step of the implicit GEMM)
 OUT_PAD = 8    # conv_out output channels padded 4 -> 8 (16-B epilogue stores)
 
@@ -454,7 +458,15 @@ class Transformer2DModel(nn.Module):
         self.proj_out = proj_out
 
     def run(self, x, nimg, HW, ctx2d, out):
-        hs = self.proj_in.run(self.norm.normalize(x, nimg, HW, False))
+        pi = self.proj_in
+        if FUSED_GN and HW >= GN_FOLD_MIN_HW and HW % 256 == 0 and x.shape[1] % 64 == 0 and not pi._forward_hooks:
+            # proj_in(GN(x)) = x . (W diag(scale_i))^T + (b + W shift_i) per image i: the normalised tensor (a full
+            # read + write of the activation) is never materialised; below 32x32 the one-launch GroupNorm is cheaper
+            scale, shift = self.norm.stats(x, nimg, HW)
+            wf, cb = ops.gn_fold(pi.weight, pi.bias, scale, shift)
+            hs = ops.linear_per_image(x, wf, cb, HW)
+        else:
+            hs = pi.run(self.norm.normalize(x, nimg, HW, False))
         for blk in self.transformer_blocks:
             hs = blk.run(hs, nimg, HW, ctx2d)
         return self.proj_out.run(hs, residual=x, out=out)

@@ -98,6 +98,23 @@ int sdmoe_groupnorm(const void* X, long ldx, int nimg, int HW, int C, int groups
                     float eps, int silu, void* Y, long ldy, float* scale, float* shift, float* workspace,
                     long workspace_floats, void* stream);
 
+/*
+ * GroupNorm folded into the linear (1x1 conv) that consumes it — Transformer2DModel.norm -> proj_in (diffusers,
+ * external): the normalised activation is never written or re-read.
+ *  sdmoe_gn_fold (per call, after sdmoe_groupnorm_stats): for each image i, Wf[i][n, k] = fp16(W[n, k] * scale[i, k])
+ *    (Wf [nimg][N][K], dense) and colbias[i][n] = bias[n] + sum_k W[n, k] * shift[i, k] (fp32 [nimg][N]; bias may
+ *    be NULL), so proj_in(GN(x)) = x . Wf[i]^T + colbias[i] on the rows of image i. K % 8 == 0, ldw % 8 == 0.
+ *  sdmoe_linear_per_image: C[m, n] = sum_k A[m, k] Wf[m / rows_per_batch][n, k] + colbias[m / rows_per_batch][n]
+ *    + R[m, n] (weights of image i at Wf + i * w_bstride elements, row stride ldw; colbias row stride
+ *    colbias_bstride). rows_per_batch % 256 == 0 (no GEMM tile straddles two images), K % 64 == 0, N % 8 == 0.
+ * Replaces sdmoe_groupnorm + sdmoe_linear of Transformer2DModel (GroupNorm(32, C) -> proj_in).
+ */
+int sdmoe_gn_fold(const void* W, long ldw, int N, int K, const void* bias, const float* scale, const float* shift,
+                  int nimg, void* Wf, float* colbias, void* stream);
+int sdmoe_linear_per_image(const void* A, long lda, const void* Wf, long ldw, long w_bstride, const float* colbias,
+                           long colbias_bstride, int rows_per_batch, const void* R, long ldr, void* C, long ldc, int M,
+                           int N, int K, float* workspace, long workspace_floats, void* stream);
+
 /* LayerNorm over the last dimension (C % 64 == 0, C <= 2048). Replaces BasicTransformerBlock norm1/2/3. */
 int sdmoe_layernorm(const void* X, long ldx, void* Y, long ldy, int M, int C, const void* gamma, const void* beta,
                     float eps, void* stream);
@@ -314,11 +331,14 @@ int sdmoe_cfg_multistep_step(const void* eps, long lde, float* lat, int B, int H
                              void* stream);
 
 /* Tuning knobs for A/B experiments: knob 0 = GEMM LDS pipeline stages (0 auto, 2 or 3); knob 1 = forced GEMM tile
-   (0 auto, 1 = 128x160, 2 = 64x160, 3 = 256x320 8-wave, 4 = 256x160 8-wave, 5 = 256x320 4x2-wave, 6 = 128x320 8-wave); knob 2 = K-step
+   (0 auto, 1 = 128x160, 2 = 64x160, 3 = 256x320 8-wave, 4 = 256x160 8-wave, 5 = 256x320 4x2-wave, 6 = 128x320 8-wave,
+   7 = 128x160 8-wave, 8 = 64x320 8-wave; 7/8 plain GEMM / conv / LN-folded GEMM only); knob 9 = forced split-K
+   factor (0 auto, 1 = never split, 2..16); knob 2 = K-step
    depth (0 auto, 32, 64); knob 3 = MFMA-cluster wave priority (0/1); knob 4 = attention kernel (0 auto by shape,
    1 = 32x32x16 MFMA kernel, 2 / 4 = 16x16x32 kernel with 32 / 64 queries per wave, 64 for head_dim <= 40
    only); knob 6 = GEMM diagnostics bits (1 no K-loop loads, 2 no MFMA, 4 no epilogue, 8 no global stores);
-   knob 7 = sdmoe_groupnorm at HW <= 256: 1 (default) statistics + apply in one launch, 0 two launches;
+   knob 7 = sdmoe_groupnorm at HW <= 256: 1 (default) statistics + apply in one launch with the rows held in
+   registers, 2 the same launch re-reading the rows for the apply, 0 two launches;
    knob 8 = GEMM residual epilogue: 1 (default) output rounded to fp16 then the residual added in fp16 arithmetic
    (diffusers' fp16 `linear(x) + residual`), 0 = accumulator + residual rounded once (fp32 staging). */
 int sdmoe_tune(int knob, int value);

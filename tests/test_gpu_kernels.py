@@ -139,7 +139,7 @@ def test_conv3x3_strided_concat_input():
     close(ops.conv3x3(buf[:, C1:], nimg, H, H, ops.conv_weight(w2), b), conv_ref(buf[:, C1:].contiguous(), nimg, H, H, w2, b))
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 4])
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 7, 8])
 def test_forced_tiles(tile):
     """Every tile configuration of the GEMM kernel (sdmoe_tune knob 1), in all three modes, with ragged M."""
     from sdmoe import _lib
@@ -157,6 +157,39 @@ def test_forced_tiles(tile):
             close(ops.conv3x3(xi, 2, H, H, ops.conv_weight(wi), bi, stride=st, upsample=up), conv_ref(xi, 2, H, H, wi, bi, st, up))
     finally:
         _lib.check(lib.sdmoe_tune(1, 0), "tune")
+
+
+@pytest.mark.parametrize("nimg,HW,C,N,mean", [(16, 4096, 320, 320, 0.0), (16, 1024, 640, 640, 0.0), (3, 256, 1280, 1280, 2.0),
+                                               (2, 1024, 640, 640, 4.0)])
+def test_gn_fold_proj_in(nimg, HW, C, N, mean):
+    """Transformer2DModel.norm -> proj_in with the GroupNorm folded into per-image weights (sdmoe_gn_fold +
+    sdmoe_linear_per_image) against GroupNorm + Linear in fp32, at the bench's 64x64 / 32x32 shapes (16 images) and
+    with a non-zero activation mean (the fold moves -mean*scale into the per-image bias)."""
+    x = rnd(nimg * HW, C, seed=50) + mean
+    gamma, beta = rnd(C, scale=0.1, seed=51) + 1, rnd(C, scale=0.1, seed=52)
+    w, b = rnd(N, C, scale=C ** -0.5, seed=53), rnd(N, scale=0.1, seed=54)
+    sc, sh = ops.groupnorm_stats(x, nimg, HW, gamma, beta, 1e-6, 32)
+    wf, cb = ops.gn_fold(w, b, sc, sh)
+    out = ops.linear_per_image(x, wf, cb, HW)
+    xn = F.group_norm(x.float().view(nimg, HW, C).permute(0, 2, 1), 32, gamma.float(), beta.float(), 1e-6)
+    ref = xn.permute(0, 2, 1).reshape(nimg * HW, C) @ w.float().t() + b.float()
+    close(out, ref)
+    # the folded weights and bias themselves
+    close(wf.float(), w.float()[None] * sc[:, None, :], rel=1e-3)
+    close(cb, b.float()[None] + sh @ w.float().t(), tol=1e-4, rel=1e-5)
+    # with a residual, and the unfused path it replaces agrees to fp16 rounding
+    r = rnd(nimg * HW, N, seed=55)
+    close(ops.linear_per_image(x, wf, cb, HW, residual=r), ref + r.float())
+    unf = ops.linear(ops.groupnorm(x, nimg, HW, gamma, beta, 1e-6, 32), w, b)
+    close(out, unf.float())
+
+
+def test_gn_fold_rejects_straddling_tiles():
+    x = rnd(2 * 100, 320, seed=56)
+    wf, cb = torch.zeros(2, 320, 320, device=DEV, dtype=torch.float16), torch.zeros(2, 320, device=DEV)
+    from sdmoe import _lib
+    with pytest.raises(_lib.SdmoeError):
+        ops.linear_per_image(x, wf, cb, 100)
 
 
 @pytest.mark.parametrize("C,HW,eps", [(320, 4096, 1e-5), (960, 256, 1e-6), (2560, 64, 1e-5), (1920, 1024, 1e-5),
@@ -305,8 +338,9 @@ def _with_tune(settings, fn):
 
 
 # tiles (sdmoe_tune knob 1): 0 auto, 1 = 128x160, 2 = 64x160, 3 = 256x320 (2x4 waves), 4 = 256x160 (4x2), 5 = 256x320
-# (4x2); stages (knob 0): 0 auto, 2, 3 -- every ring the M = 65,536 problems can take
-FULL_TILES = [(t, s) for t in (0, 1, 2, 3, 4, 5) for s in (0, 2, 3)]
+# (4x2), 7 = 128x160 (4x2, 8 waves), 8 = 64x320 (2x4, 8 waves); stages (knob 0): 0 auto, 2, 3 -- every ring the
+# M = 65,536 problems can take
+FULL_TILES = [(t, s) for t in (0, 1, 2, 3, 4, 5, 7, 8) for s in (0, 2, 3)]
 
 
 @pytest.mark.parametrize("tile,stages", FULL_TILES)
@@ -358,9 +392,11 @@ def test_groupnorm_full_size(C, HW):
     close(y, F.silu(ref.permute(0, 2, 1).reshape(nimg * HW, C)), tol=5e-3)
 
 
-def test_geglu_fused_full_size():
+@pytest.mark.parametrize("tile", [0, 1, 7])
+def test_geglu_fused_full_size(tile):
     """The 64x64 level's fused projection + ReLU GEGLU + expert scores at M = 65,536 (F = 1280, 64 experts of 20)
-    against the unfused projection GEMM + route kernel: bit-identical."""
+    against the unfused projection GEMM + route kernel: bit-identical, on the auto tile and the 128x160 4- and
+    8-wave tiles."""
     M, C, E = 65536, 320, 64
     F_ = 4 * C
     g = torch.Generator().manual_seed(77)
@@ -370,7 +406,10 @@ def test_geglu_fused_full_size():
     routing = ops.Routing(torch.randperm(F_, generator=g) % E, E, 12, DEV)
     w_il, b_il = ops.interleave_geglu(w, b, routing.perm)
     score = torch.empty((M, E), dtype=torch.float16, device=DEV)
-    P = ops.linear_geglu(x, w_il, b_il, ops.ACT_RELU, score=score, esize=routing.esize)
+    res = []
+    _with_tune([(1, tile)], lambda: res.append(ops.linear_geglu(x, w_il, b_il, ops.ACT_RELU, score=score,
+                                                                esize=routing.esize)))
+    P = res[0]
     score_u = torch.empty_like(score)
     out_u = ops.geglu_route(ops.linear(x, w, b), routing, ops.ACT_RELU, score_out=score_u, k=E)
     assert torch.equal(score, score_u)
@@ -480,16 +519,17 @@ def test_groupnorm_small_bench_shapes(H, C):
                                             (64, 1280, 16, True), (64, 2560, 16, True), (64, 1280, 3, False),
                                             (16, 128, 2, True), (1024, 960, 2, True)])
 def test_groupnorm_single_launch_bit_identical(HW, C, nimg, silu):
-    """gn_fused_kernel (statistics + apply in one launch, HW <= 1024) vs the two-launch path (gn_small_kernel +
-    gn_apply_kernel, sdmoe_tune knob 7 = 0): the same sums in the same order, the same fp64 finalize and the same
-    fp32 scale/shift, so output AND the returned scale/shift are bit-identical; strided input/output views."""
+    """The single-launch kernels (statistics + apply, HW <= 256: gn_fused_reg_kernel, knob 7 = 1, and
+    gn_fused_kernel, knob 7 = 2) vs the two-launch path (gn_small_kernel + gn_apply_kernel, knob 7 = 0): the same
+    sums in the same order, the same fp64 finalize and the same fp32 scale/shift, so the outputs are bit-identical;
+    strided input/output views."""
     from sdmoe import _lib
     lib = _lib.load()
     buf = rnd(nimg * HW, C + 64, seed=HW + C) * 2 + 1
     x = buf[:, 64:]
     gamma, beta = rnd(C, scale=0.1, seed=C + 1) + 1, rnd(C, scale=0.1, seed=C + 2)
     outs = []
-    for mode in (1, 0):
+    for mode in (1, 2, 0):
         _lib.check(lib.sdmoe_tune(7, mode), "tune")
         try:
             dst = torch.full((nimg * HW, C + 16), 7.0, dtype=torch.float16, device=DEV)
@@ -497,7 +537,7 @@ def test_groupnorm_single_launch_bit_identical(HW, C, nimg, silu):
             outs.append(dst)
         finally:
             _lib.check(lib.sdmoe_tune(7, 1), "tune")
-    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[0], outs[2]) and torch.equal(outs[1], outs[2])
     assert (outs[0][:, :8] == 7).all() and (outs[0][:, 8 + C:] == 7).all()
     ref = F.group_norm(x.float().reshape(nimg, HW, C).permute(0, 2, 1), 32, gamma.float(), beta.float(), 1e-5)
     ref = ref.permute(0, 2, 1).reshape(nimg * HW, C)
