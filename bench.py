@@ -56,6 +56,9 @@ def parse():
                    help="after the timed metric run, time this many end-to-end steps (text encoder + denoise + VAE "
                         "decode to RGB) and report them as 'end_to_end' (0: skip)")
     p.add_argument("--no-roofline", action="store_true")
+    p.add_argument("--roofline-sample", type=int, default=25,
+                   help="time the conv launches of every N-th U-Net evaluation (1 = every launch; event markers idle "
+                        "the GPU ~5.7 us each)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-evals", type=int, default=2, help="CPU oracle U-Net evaluations to time")
     p.add_argument("--cpu-full-image", action="store_true",
@@ -183,21 +186,48 @@ def build(args, world, rank, dev):
 
 
 class KernelTimer:
-    """HIP-event timing of every launch of one kernel family on the stream it is launched on."""
+    """HIP-event timing of the launches of one kernel family on the stream it is launched on, over the timed region.
 
-    def __init__(self, family):
+    Sampled by U-Net evaluation: every `sample_every`-th evaluation of the timed steps has ALL its launches of the
+    family bracketed by an event pair (2 of the 50 evaluations of a step: all 52 conv shapes each); the others run
+    untouched. Each event record is a marker packet that idles the GPU for ~5.7 us between kernels (rocprofv3 kernel
+    trace: a gap at every conv boundary, 0.6 ms per evaluation when all 104 records per evaluation were taken), so
+    timing every launch slowed the very step it measures: 9.12 images/s timed at every launch vs 9.28 at every 10th
+    evaluation vs 9.30 untimed (same box, same conv average 1.02-1.03 PFLOP/s)."""
+
+    def __init__(self, family, sample_every=25):
         self.family = family
         self.pairs = []
         self.flops = 0.0
         self.bytes = 0.0
         self.active = False
+        self.sample_every = max(1, int(sample_every))
+        self.evals = 0
+        self.sampled_evals = 0
+        self.on_eval = False
+
+    def wrap_evals(self, unet):
+        """Count U-Net evaluations (forward_nhwc) while active; launches are timed only in sampled evaluations."""
+        orig = unet.forward_nhwc
+        timer = self
+
+        def wrapped(*a, **k):
+            if timer.active:
+                timer.on_eval = timer.evals % timer.sample_every == 0
+                timer.sampled_evals += int(timer.on_eval)
+                timer.evals += 1
+            try:
+                return orig(*a, **k)
+            finally:
+                timer.on_eval = False
+        unet.forward_nhwc = wrapped
 
     def wrap(self, ops_mod):
         orig = getattr(ops_mod, self.family)
         timer = self
 
         def wrapped(*a, **k):
-            if not timer.active:
+            if not (timer.active and timer.on_eval):
                 return orig(*a, **k)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
@@ -327,9 +357,10 @@ def main():
     from sdmoe import distributed as D
     prompts = [f"synthetic prompt {i}" for i in range(world * args.batch)]
 
-    timer = KernelTimer("conv3x3_launch")
+    timer = KernelTimer("conv3x3_launch", args.roofline_sample)
     if not args.no_roofline:
         timer.wrap(ops)
+        timer.wrap_evals(pipe.unet)
     pipe.unet.conv_in.weight._sdmoe_conv_in = True
     pipe.unet.conv_out.weight._sdmoe_conv_out = True
 
@@ -406,6 +437,8 @@ def main():
                     "achieved": round(achieved, 1), "peak": PEAK_FP16_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(achieved / PEAK_FP16_TFLOPS, 4), "traffic": traffic, "traffic_source": traffic_src,
                     "launches": n, "avg_launch_ms": round(ms / n, 4),
+                    "sampled": f"HIP events around every conv launch of every {timer.sample_every}th U-Net evaluation "
+                               f"of the timed steps ({timer.sampled_evals} of {timer.evals})",
                     "algorithmic_flop_per_launch": round(flops / n)}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.model == "sd14":

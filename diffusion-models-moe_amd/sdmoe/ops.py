@@ -17,7 +17,16 @@ ACT_NONE, ACT_SILU, ACT_GELU, ACT_RELU, ACT_QUICK_GELU = 0, 1, 2, 3, 4
 ACT_BY_NAME = {"none": ACT_NONE, "silu": ACT_SILU, "gelu": ACT_GELU, "relu": ACT_RELU, "quick_gelu": ACT_QUICK_GELU}
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_cur_dev = getattr(torch._C, "_cuda_getDevice", None)
+
+
 def _stream():
+    """hipStream_t of torch's current stream on the current device. The C accessors skip the Python Stream object
+    and device-index resolution of torch.cuda.current_stream() (2.7 us -> ~0.3 us per launch; ~370 launches per
+    U-Net evaluation)."""
+    if _raw_stream is not None and _cur_dev is not None:
+        return _raw_stream(_cur_dev())
     return torch.cuda.current_stream().cuda_stream
 
 

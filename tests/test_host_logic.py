@@ -476,3 +476,27 @@ def test_sdmoe_tune_env_is_parsed_at_load(monkeypatch):
     monkeypatch.setattr(_lib, "_lib", None)
     monkeypatch.delenv("SDMOE_TUNE")
     _lib.load()
+
+
+def test_bench_roofline_timer_samples_whole_evaluations():
+    """bench.KernelTimer times the conv launches of every N-th U-Net evaluation only (event markers idle the GPU
+    between kernels): on_eval is set for evaluations 0, N, 2N, ... of the active region and nowhere else."""
+    import bench
+
+    seen = []
+
+    class FakeUNet:
+        def forward_nhwc(self, *a, **k):
+            seen.append(timer.on_eval)
+
+    timer = bench.KernelTimer("conv3x3_launch", sample_every=10)
+    u = FakeUNet()
+    timer.wrap_evals(u)
+    u.forward_nhwc()  # inactive: not counted
+    timer.active = True
+    for _ in range(25):
+        u.forward_nhwc()
+    timer.active = False
+    assert seen[0] is False
+    assert [i for i, on in enumerate(seen[1:]) if on] == [0, 10, 20]
+    assert timer.evals == 25 and timer.sampled_evals == 3 and timer.on_eval is False
