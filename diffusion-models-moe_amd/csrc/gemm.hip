@@ -38,6 +38,7 @@ int g_bk = 0;
 int g_prio = 0;
 int g_res16 = 1;  // knob 8: 1 = residual epilogues on the fp16 staging path (residual added in the copy-out), 0 = fp32
 int g_ksplit = 0;  // knob 9: forced split-K factor (0 = auto; 1 = never split), for tile sweeps
+int g_mfast = 1;   // knob 14: split-K conv grids ordered M-tile fastest (1) or split fastest (0)
 int g_diag = 0;  // knob 6, diagnostics only (results garbage): bit 0 = no K-loop operand loads, bit 1 = no MFMAs,
                  // bit 2 = no epilogue (nothing stored), bit 3 = epilogue without its global stores
 
@@ -57,6 +58,7 @@ struct GemmParams {
   int rows_per_batch;
   int H, Wd, Cin, OH, OW, stride, upsample;
   int ksplit, kchunk;
+  int mfast;  // tile order M-fastest (split-K grids, sdmoe_tune knob 14)
   int a_bytes, w_bytes;  // SRD num_records
   // routed-GEGLU epilogue (sdmoe_linear_geglu): W rows interleaved [value 8 | gate 8] per 8-neuron chunk, C is
   // the [M, N/2] product value * act(gate); score [M, ld_score] gets per-expert sums of act(gate) over
@@ -243,8 +245,20 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
   const int wr = wave / WNW, wc = wave % WNW;
   const int ntn = (p.N + BN - 1) / BN, ntm = (p.M + BM - 1) / BM;
   const int bid = xcd_remap(blockIdx.x, ntn * ntm * p.ksplit);
-  const int split = bid % p.ksplit, tile = bid / p.ksplit;
-  const int tn = tile % ntn, tm = tile / ntn;
+  // tile order: (split, N-tile, M-tile) with the split fastest, or -- split-K grids under mfast -- the M-tile
+  // fastest, so the workgroups xcd_remap puts on one XCD share (N-tile, split) weight slices in that XCD's L2
+  int split, tn, tm;
+  if (p.mfast) {
+    tm = bid % ntm;
+    const int r = bid / ntm;
+    tn = r % ntn;
+    split = r / ntn;
+  } else {
+    split = bid % p.ksplit;
+    const int tile = bid / p.ksplit;
+    tn = tile % ntn;
+    tm = tile / ntn;
+  }
   const int m0 = tm * BM, n0 = tn * BN;
   const int nk_total = p.K / BK;
   const int ks0 = split * p.kchunk;
@@ -827,6 +841,10 @@ int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
   constexpr int NTH = 64 * WMW * WNW;
   p.kchunk = (nk + p.ksplit - 1) / p.ksplit;
   p.part = p.ksplit > 1 ? ws : nullptr;
+  // M-fastest order for split-K convs only: their weight slices (up to 29 MB at the 16x16 level) were re-fetched by
+  // every XCD (PMC FETCH_SIZE of the split-K conv launches 140 -> 46 MB, time neutral); the M = 1024 split-K linears
+  // measured 2 us slower with it
+  p.mfast = (p.ksplit > 1 && g_mfast && (MODE == MODE_CONV || MODE == MODE_CONV_UP)) ? 1 : 0;
   p.prio = g_prio;
   p.diag = g_diag;
   p.res16 = g_res16;
@@ -1313,6 +1331,7 @@ extern "C" int sdmoe_tune(int knob, int value) {
   if (knob == 0 && (value == 0 || value == 2 || value == 3)) { g_stages = value; return SDMOE_OK; }
   if (knob == 1 && value >= 0 && value <= 8) { g_tile = value; return SDMOE_OK; }
   if (knob == 9 && value >= 0 && value <= 16) { g_ksplit = value; return SDMOE_OK; }
+  if (knob == 14 && (value == 0 || value == 1)) { g_mfast = value; return SDMOE_OK; }
   if (knob == 2 && (value == 0 || value == 32 || value == 64)) { g_bk = value; return SDMOE_OK; }
   if (knob == 3 && (value == 0 || value == 1)) { g_prio = value; return SDMOE_OK; }
   if (knob == 6 && value >= 0 && value <= 15) { g_diag = value; return SDMOE_OK; }

@@ -333,7 +333,8 @@ int sdmoe_cfg_multistep_step(const void* eps, long lde, float* lat, int B, int H
 /* Tuning knobs for A/B experiments: knob 0 = GEMM LDS pipeline stages (0 auto, 2 or 3); knob 1 = forced GEMM tile
    (0 auto, 1 = 128x160, 2 = 64x160, 3 = 256x320 8-wave, 4 = 256x160 8-wave, 5 = 256x320 4x2-wave, 6 = 128x320 8-wave,
    7 = 128x160 8-wave, 8 = 64x320 8-wave; 7/8 plain GEMM / conv / LN-folded GEMM only); knob 9 = forced split-K
-   factor (0 auto, 1 = never split, 2..16); knob 2 = K-step
+   factor (0 auto, 1 = never split, 2..16); knob 14 = split-K conv tile order: 1 (default) M-tile fastest (one XCD's
+   workgroups share weight slices in its L2), 0 split fastest; knob 2 = K-step
    depth (0 auto, 32, 64); knob 3 = MFMA-cluster wave priority (0/1); knob 4 = attention kernel (0 auto by shape,
    1 = 32x32x16 MFMA kernel, 2 / 4 = 16x16x32 kernel with 32 / 64 queries per wave, 64 for head_dim <= 40
    only); knob 6 = GEMM diagnostics bits (1 no K-loop loads, 2 no MFMA, 4 no epilogue, 8 no global stores);
