@@ -60,6 +60,17 @@ def key_flops(name, a, k, out):
         return (f"topk_mask {tuple(P.shape)}", 0, P.numel() * 4)
     if name == "add":
         return (f"add {tuple(a[0].shape)}", 0, a[0].numel() * 6)
+    if name == "moe_topk_keep":
+        sc, routing, M = a[0], a[1], a[2]
+        return (f"topk_keep {tuple(sc.shape)}", 0, sc.numel() * 2 + M * routing.E * routing.esize // 8)
+    if name == "linear_per_image":
+        x, wf = a[0], a[1]
+        M, K = x.shape
+        N = wf.shape[1]
+        return (f"linear_per_image (GN-folded proj_in) M={M} N={N} K={K}", 2.0 * M * N * K, 0)
+    if name == "gn_fold":
+        nimg, N, K = a[2].shape[0], a[0].shape[0], a[0].shape[1]
+        return (f"gn_fold nimg={nimg} N={N} K={K}", 0, nimg * N * K * 2)
     return (name, 0, 0)
 
 
@@ -89,7 +100,8 @@ def main():
     ap.add_argument("--evals", type=int, default=2)
     a = ap.parse_args()
     for n in ("conv3x3_launch", "linear", "linear_ln", "linear_geglu", "linear_keep", "groupnorm", "attention", "groupnorm_stats", "groupnorm_apply",
-              "layernorm", "moe_topk_mask", "add", "mask_weight", "geglu_route"):
+              "layernorm", "moe_topk_mask", "moe_topk_keep", "add", "mask_weight", "geglu_route", "gn_fold",
+              "linear_per_image"):
         wrap(n)
     from sdmoe.config import UNetConfig
     from sdmoe.pipeline import StableDiffusionPipeline
