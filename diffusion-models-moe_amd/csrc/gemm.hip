@@ -821,14 +821,14 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
 }
 
 template <int BM, int BN, int WMW, int WNW, int MODE>
-int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
+int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s, int ks_want = 0, int stages_want = 0) {
   const int ntiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
   const int nk = p.K / 64;
   if (p.w_bstride && p.rows_per_batch % BM) return SDMOE_EUNSUP;  // a tile would straddle two images' weights
   int ksplit = 1;
   // fill the chip: split K when the tile grid covers well under one wave of 256 CUs
-  if (ws && g_ksplit > 0) {
-    ksplit = g_ksplit;
+  if (ws && (g_ksplit > 0 || ks_want > 0)) {
+    ksplit = g_ksplit > 0 ? g_ksplit : ks_want;
     if (ksplit > nk) ksplit = nk;
     while (ksplit > 1 && (long)ksplit * p.M * p.N > ws_floats) --ksplit;
   } else if (ws && ntiles < 192 && nk >= 16) {
@@ -853,7 +853,8 @@ int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
     // 64-deep K-steps (a 32-deep 4/5-stage ring measured slower on every shape; the kernel is generic in BK).
     // 4-wave tiles: 2-stage ring (2 workgroups/CU) when the grid has >= ~300 workgroups, else 3-stage; 8-wave
     // tiles: 3-stage where it fits in LDS -- measured crossovers on MI355X.
-    const int stages = g_stages ? g_stages : ((WMW * WNW == 4 && ntiles * p.ksplit >= 300) ? 2 : 3);
+    const int stages = g_stages ? g_stages
+                                : (stages_want ? stages_want : ((WMW * WNW == 4 && ntiles * p.ksplit >= 300) ? 2 : 3));
     constexpr bool FITS3 = 3 * ((BM + BN) * 64 * 2 + 1024 + keep_stage_bytes<BM, BN, MODE>()) +
                                (keep_stage_bytes<BM, BN, MODE>() ? KEEP_LUT_BYTES : 0) +
                                ((MODE == MODE_GEMM_LN || MODE == MODE_GEGLU_LN) ? BM * 8 + BN * 8 : 0) <= 160 * 1024;
@@ -941,6 +942,10 @@ int dispatch(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
   // 64x64 -> 32x32 stride-2 conv (M = 16384, N = 320) on 64x160 tiles at two workgroups per CU: 38 vs 57 us on
   // 128x160 with a 3-stage ring
   if constexpr (MODE == MODE_CONV) {
+    // 8x8-level 3x3 convs (M = 1024, K = 9 x 1280 / 9 x 2560): 8-wave 128x160 tiles (wave tile 32x80), 2-stage ring
+    // (two workgroups per CU), 8-way split-K: 44.6 / 68.2 us vs 51.2 / 72.8 on 256x160 4x2 waves (tile_sweep.py)
+    if (p.stride == 1 && p.N % 160 == 0 && p.M <= 1024 && p.K >= 9 * 1280)
+      return launch_tile<128, 160, 4, 2, MODE>(p, ws, ws_floats, s, 8, 2);
     if (p.stride == 1 && p.N % 320 == 0 && nt320 < 240 && p.K >= 9 * 1280 && p.M >= 2048 && p.M <= 4096)
       return launch_tile<256, 320, 2, 4, MODE>(p, ws, ws_floats, s);
     if (p.stride == 2 && p.N % 160 == 0 && p.M >= 8192) return launch_tile<64, 160, 2, 2, MODE>(p, ws, ws_floats, s);
