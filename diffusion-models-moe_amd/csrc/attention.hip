@@ -55,8 +55,8 @@ SDMOE_DEV void bld16(__amdgpu_buffer_rsrc_t rs, const half_t* lds_dst, unsigned 
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)lds_dst, 16, voff, 0, 0, 0);
 }
 
-template <int D, int NQF>
-__global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn_fwd_kernel(AttnParams p) {
+template <int D, int NQF, int NW = 4>
+__global__ __launch_bounds__(NW * 64, (D >= 160 || NW >= 8 ? 1 : 2)) void attn_fwd_kernel(AttnParams p) {
   constexpr int DK = ((D + 31) / 32) * 32;   // contraction dim padded for 16x16x32
   constexpr int DV = ((D + 15) / 16) * 16;   // output dim padded to 16-row fragments
   constexpr int KB = 64;                      // keys per tile
@@ -70,8 +70,7 @@ __global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn_fwd_kernel(AttnP
   constexpr int SL = RS / 8;                  // 16-B LDS slots per row (SL - CH padding slots, loaded as zeros)
   constexpr int TILE = KB * RS;               // halves per K (or V) tile image
   constexpr int NPIECE = TILE * 2 / 1024;     // 1-KiB LDS-DMA wave-instructions per K (or V) tile
-  constexpr int NPW = 2 * NPIECE / 4;         // per wave, K and V together
-  static_assert((2 * NPIECE) % 4 == 0, "K+V pieces must split evenly over the 4 waves");
+  constexpr int NPW = (2 * NPIECE + NW - 1) / NW;  // per wave, K and V together (the last round may be partial)
   constexpr int KBUF = TILE + 64;             // + zeroed tail for the over-read of the last K row
   constexpr bool SUM_BY_MFMA = DV > D;        // O^T row D accumulates sum_k P[k][q] (V column D := 1.0)
   static_assert(!SUM_BY_MFMA || D % 16 == 8, "ones column sits at the start of a 4-column tr-read group");
@@ -89,7 +88,7 @@ __global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn_fwd_kernel(AttnP
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, w = lane & 15;
   const int b = blockIdx.z, h = blockIdx.y;
-  const int q0 = blockIdx.x * (64 * NQF) + wave * (16 * NQF);
+  const int q0 = blockIdx.x * (NW * 16 * NQF) + wave * (16 * NQF);
 
   const half_t* Qb = p.Q + (long)b * p.Nq * p.ldq + h * D;
   const half_t* Kb = p.K + (long)b * p.Nk * p.ldk + h * D;
@@ -100,12 +99,12 @@ __global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn_fwd_kernel(AttnP
   const __amdgpu_buffer_rsrc_t rsV =
       __builtin_amdgcn_make_buffer_rsrc((void*)Vb, (short)0, (int)(((long)p.Nk - 1) * p.ldv * 2 + D * 2), 0x00020000);
 
-  // per-wave LDS-DMA pieces: global piece gp = wave + 4j (K pieces first, then V); lane = one 16-B slot
+  // per-wave LDS-DMA pieces: global piece gp = wave + NW j (K pieces first, then V); lane = one 16-B slot
   unsigned voff[NPW], vstep[NPW];
   int ldsoff[NPW];
 #pragma unroll
   for (int j = 0; j < NPW; ++j) {
-    const int gp = wave + 4 * j;
+    const int gp = wave + NW * j;
     const bool isk = gp < NPIECE;
     const int pc = isk ? gp : gp - NPIECE;
     const int slot = pc * 64 + lane, r = slot / SL, c = slot - (slot / SL) * SL;
@@ -117,13 +116,14 @@ __global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn_fwd_kernel(AttnP
   auto issue_tile = [&](half_t* Sd) {  // DMA the tile at the current voff into ring slot Sd, advance voff
 #pragma unroll
     for (int j = 0; j < NPW; ++j) {
-      bld16(wave + 4 * j < NPIECE ? rsK : rsV, Sd + ldsoff[j], voff[j]);
+      if ((2 * NPIECE) % NW == 0 || wave + NW * j < 2 * NPIECE)  // wave-uniform
+        bld16(wave + NW * j < NPIECE ? rsK : rsV, Sd + ldsoff[j], voff[j]);
       voff[j] += vstep[j];
     }
   };
 
   // zeroed over-read tails, the constant [1 0 0 0 | 0 0 0 0] block the V^T reads of the ones column use
-  for (int i = tid; i < KBUF - TILE; i += 256) S0[TILE + i] = S1[TILE + i] = 0;
+  for (int i = tid; i < KBUF - TILE; i += NW * 64) S0[TILE + i] = S1[TILE + i] = 0;
   if (tid < 8) S0[KBUF + TILE + tid] = S1[KBUF + TILE + tid] = (half_t)(tid == 0 ? 1.f : 0.f);
 
   const int nkt = (p.Nk + KB - 1) / KB;
@@ -211,13 +211,16 @@ __global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn_fwd_kernel(AttnP
       float m4 = max3(s[f][3][0], s[f][3][1], s[f][3][2]);
       m0 = max3(m0, m1, s[f][3][3]);
       m2 = max3(m2, m3, m4);
-      const float mx = max_xrows(max2(m0, m2));
+      // lane-local max: the wave-uniform rescale test needs no cross-lane step (all lane maxima <= THR iff all row
+      // maxima are); the row max over the 4 lanes of a query (l, l^16, l^32, l^48) only where m moves
+      const float ml = max2(m0, m2);
       if (kt == 0) {  // first tile: m = its max (O and l are still zero)
+        const float mx = max_xrows(ml);
         mrun[f] = mx;
 #pragma unroll
         for (int kf = 0; kf < 4; ++kf) s[f][kf] -= mx;
-      } else if (!__all(mx <= RESCALE_THR)) {  // wave-uniform decision
-        const float delta = fmaxf(mx, 0.f);
+      } else if (!__all(ml <= RESCALE_THR)) {  // wave-uniform decision
+        const float delta = fmaxf(max_xrows(ml), 0.f);
         mrun[f] += delta;
         const float alpha = __builtin_amdgcn_exp2f(-delta);
         if (!SUM_BY_MFMA) lrun[f] *= alpha;
@@ -565,8 +568,10 @@ __global__ __launch_bounds__(256, (D <= 40 ? 4 : (D >= 160 ? 1 : 2))) void attn3
     }
 }
 
-// sdmoe_tune knob 4: 0 = by shape (default): attn32_kernel for d = 80 self-attention (Nk > 128), the 16x16x32
-// kernel (NQF = 2) everywhere else; 1 = attn32_kernel; 2 or 4 = the 16x16x32 kernel with NQF = 2 / 4
+// sdmoe_tune knob 4: 0 = by shape (default): attn32_kernel for d = 80 self-attention (Nk > 128), the 16x16x32 kernel
+// in 8-wave workgroups for d = 40 / 64 self-attention (Nk > 128), the 4-wave 16x16x32 kernel (NQF = 2) everywhere
+// else; 1 = attn32_kernel; 2 or 4 = the 4-wave 16x16x32 kernel with NQF = 2 / 4; 8 / 16 = the 16x16x32 kernel in
+// 8-wave (d <= 80) / 16-wave (d <= 40) workgroups
 int g_attn_nqf = 0;
 
 template <int D>
@@ -582,12 +587,22 @@ int launch(const AttnParams& p, int nimg, hipStream_t s) {
   // (14 MFMAs and ~100 VALU per 64-key tile vs 28 and ~110 at d = 40) but runs slower: lower clock under DVFS for
   // the 32x32 MFMA (MI355X_MICROARCH.md) and 2-way LDS bank conflicts on its V^T transpose reads (row stride 56)
   const bool use32 = g_attn_nqf == 1 || (g_attn_nqf == 0 && D == 80 && p.Nk > 128);
+  // 8-wave workgroups (256 queries share each K/V tile: half the LDS-DMA pieces per wave and tile) for the long
+  // self-attentions at d = 40 / 64: d = 40 N = 4096 448 vs 464-475 us, pipeline +0.5 % (same box); slower on the
+  // 77-key cross-attention (34.4 vs 31.1 us: fewer workgroups) and at d = 80 (65.4 vs 62.4 us with attn32)
+  const bool use8 = g_attn_nqf == 8 || (g_attn_nqf == 0 && (D == 40 || D == 64) && p.Nk > 128);
   if (use32) {
     dim3 grid((p.Nq + 127) / 128, p.heads, nimg);
     attn32_kernel<D><<<grid, 256, 0, s>>>(p);
   } else if (WIDE_OK && wide) {
     dim3 grid((p.Nq + 255) / 256, p.heads, nimg);
     attn_fwd_kernel<D, (WIDE_OK ? 4 : 2)><<<grid, 256, 0, s>>>(p);
+  } else if (use8 && D <= 80) {
+    dim3 grid((p.Nq + 255) / 256, p.heads, nimg);
+    attn_fwd_kernel<D, 2, (D <= 80 ? 8 : 4)><<<grid, (D <= 80 ? 512 : 256), 0, s>>>(p);
+  } else if (g_attn_nqf == 16 && D <= 40) {
+    dim3 grid((p.Nq + 511) / 512, p.heads, nimg);
+    attn_fwd_kernel<D, 2, (D <= 40 ? 16 : 4)><<<grid, (D <= 40 ? 1024 : 256), 0, s>>>(p);
   } else {
     dim3 grid((p.Nq + 127) / 128, p.heads, nimg);
     attn_fwd_kernel<D, 2><<<grid, 256, 0, s>>>(p);
@@ -599,7 +614,7 @@ int launch(const AttnParams& p, int nimg, hipStream_t s) {
 }  // namespace
 
 int sdmoe_attn_set_nqf(int v) {
-  if (v != 0 && v != 1 && v != 2 && v != 4) return SDMOE_EARG;
+  if (v != 0 && v != 1 && v != 2 && v != 4 && v != 8 && v != 16) return SDMOE_EARG;
   g_attn_nqf = v;
   return SDMOE_OK;
 }

@@ -264,6 +264,31 @@ def test_attention(d, Nq, Nk):
     close(out, ref)
 
 
+@pytest.mark.parametrize("variant", [1, 2, 4, 8, 16])
+@pytest.mark.parametrize("d,Nq,Nk", [(40, 256, 256), (40, 300, 77), (80, 200, 200), (64, 300, 300),
+                                     (32, 130, 130)])
+def test_attention_forced_variant(variant, d, Nq, Nk):
+    """Every attention kernel variant (sdmoe_tune knob 4: 1 = 32x32x16 kernel, 2 / 4 = 16x16x32 kernel with 32 / 64
+    queries per wave, 8 = 16x16x32 kernel in 8-wave workgroups), ragged Nq and Nk."""
+    from sdmoe import _lib
+    lib = _lib.load()
+    nimg, heads = 2, 4
+    C = heads * d
+    q = rnd(nimg * Nq, C, seed=60)
+    kv = rnd(nimg * Nk, 2 * C, seed=61)
+    k, v = kv[:, :C], kv[:, C:]
+    _lib.check(lib.sdmoe_tune(4, variant), "tune")
+    try:
+        out = ops.attention(q, k, v, nimg, Nq, Nk, heads)
+    finally:
+        _lib.check(lib.sdmoe_tune(4, 0), "tune")
+    qf = q.float().reshape(nimg, Nq, heads, d).transpose(1, 2)
+    kf = k.float().reshape(nimg, Nk, heads, d).transpose(1, 2)
+    vf = v.float().reshape(nimg, Nk, heads, d).transpose(1, 2)
+    ref = F.scaled_dot_product_attention(qf, kf, vf).transpose(1, 2).reshape(nimg * Nq, C)
+    close(out, ref)
+
+
 def test_attention_peaked_softmax():
     """A spiked key forces the online-softmax rescale branch at a later tile."""
     nimg, heads, d, N = 1, 8, 80, 512
