@@ -50,12 +50,25 @@ SDMOE_DEV float max_xrows(float v) {
   return max2(__uint_as_float(t[0]), __uint_as_float(t[1]));
 }
 
+// 2^x for x <= 8 (softmax arguments after the running-max shift): n = rint(x) by the 1.5 * 2^23 magic add, f = x - n
+// in [-0.5, 0.5], 2^f by a degree-3 near-minimax polynomial (max rel. error 2.2e-4, inside fp16's 2^-11 rounding of P), the
+// exponent added to the bit pattern; x below -126 clamps to 2^-126 (P then rounds to 0 in fp16 as v_exp's result does)
+SDMOE_DEV float exp2_poly(float x) {
+  x = fmaxf(x, -126.f);
+  const float t = x + 12582912.f;
+  const float f = x - (t - 12582912.f);
+  float q = __builtin_fmaf(f, 0.05286744f, 0.24215189f);
+  q = __builtin_fmaf(f, q, 0.69358675f);
+  q = __builtin_fmaf(f, q, 0.99996276f);
+  return __uint_as_float(__float_as_uint(q) + (__float_as_uint(t) << 23));
+}
+
 typedef __attribute__((address_space(3))) void lds_void_t;
 SDMOE_DEV void bld16(__amdgpu_buffer_rsrc_t rs, const half_t* lds_dst, unsigned voff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)lds_dst, 16, voff, 0, 0, 0);
 }
 
-template <int D, int NQF, int NW = 4>
+template <int D, int NQF, int NW = 4, int POLY = 0>
 __global__ __launch_bounds__(NW * 64, (D >= 160 || NW >= 8 ? 1 : 2)) void attn_fwd_kernel(AttnParams p) {
   constexpr int DK = ((D + 31) / 32) * 32;   // contraction dim padded for 16x16x32
   constexpr int DV = ((D + 15) / 16) * 16;   // output dim padded to 16-row fragments
@@ -79,10 +92,14 @@ __global__ __launch_bounds__(NW * 64, (D >= 160 || NW >= 8 ? 1 : 2)) void attn_f
 
   // separate arrays per ring slot: with the slot a compile-time constant the compiler can tell the DMA into
   // one slot from the ds_reads of the other and does not drain vmcnt in front of every LDS read
-  // slot layout: [K tile | zero tail | V tile | 1 0 0 0 0 0 0 0]
-  constexpr int SLOT = KBUF + TILE + 8;
+  // slot layout: [K tile | zero tail | V tile]
+  constexpr int SLOT = KBUF + TILE;
   __shared__ __attribute__((aligned(1024))) half_t S0[SLOT];
   __shared__ __attribute__((aligned(1024))) half_t S1[SLOT];
+  // the ones column's V^T operand: 16 rows of [1 0 0 0] at a 32-B row stride, offset 16 B into each row, so the 16
+  // lanes that read it take banks 4-5 (mod 8) of distinct 8-bank groups, beside the V-tile lanes' banks 0-3 and 6-7
+  // of the same read (a single shared [1 0 0 0] block read by all 16 lanes cost 2 conflict cycles per read)
+  __shared__ __attribute__((aligned(1024))) half_t ONES[SUM_BY_MFMA ? 16 * 16 : 1];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -124,7 +141,8 @@ __global__ __launch_bounds__(NW * 64, (D >= 160 || NW >= 8 ? 1 : 2)) void attn_f
 
   // zeroed over-read tails, the constant [1 0 0 0 | 0 0 0 0] block the V^T reads of the ones column use
   for (int i = tid; i < KBUF - TILE; i += NW * 64) S0[TILE + i] = S1[TILE + i] = 0;
-  if (tid < 8) S0[KBUF + TILE + tid] = S1[KBUF + TILE + tid] = (half_t)(tid == 0 ? 1.f : 0.f);
+  if constexpr (SUM_BY_MFMA)
+    for (int i = tid; i < 16 * 16; i += NW * 64) ONES[i] = (half_t)(i % 16 == 8 ? 1.f : 0.f);
 
   const int nkt = (p.Nk + KB - 1) / KB;
   issue_tile(S0);
@@ -153,12 +171,12 @@ __global__ __launch_bounds__(NW * 64, (D >= 160 || NW >= 8 ? 1 : 2)) void attn_f
 #pragma unroll
   for (int f = 0; f < NQF; ++f) mrun[f] = lrun[f] = 0.f;
 
-  // V^T fragment addresses (tr reads, key slots permuted to match P); lanes of the ones-column group read the
-  // constant block instead
+  // V^T fragment addresses (tr reads, key slots permuted to match P); the lanes of the ones column read the ONES
+  // rows instead, the lanes past it the V tile's zero-loaded padding columns
   const int tq = w >> 2, tp = w & 3;
   auto vaddr = [&](const half_t* Vt, int c2, int hi, int df) -> const half_t* {
     const int normal = (32 * c2 + 16 * hi + 4 * g + tq) * RS + 16 * df + 4 * tp;
-    if (SUM_BY_MFMA && df == D / 16) return Vt + (4 * tp >= D % 16 ? TILE + (4 * tp == D % 16 ? 0 : 4) : normal);
+    if (SUM_BY_MFMA && df == D / 16 && 4 * tp == D % 16) return ONES + (4 * g + tq) * 16 + 8;
     return Vt + normal;
   };
 
@@ -234,7 +252,12 @@ __global__ __launch_bounds__(NW * 64, (D >= 160 || NW >= 8 ? 1 : 2)) void attn_f
       for (int kf = 0; kf < 4; ++kf)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float e = __builtin_amdgcn_exp2f(s[f][kf][i]);
+          // POLY (evaluation variant, sdmoe_tune knob 4 = 40): the last 16-key column block's exp2 as a Cody-Waite
+          // reduction + degree-3 polynomial on the FMA pipe (8 plain VALU issues in place of one v_exp). Measured
+          // slower, so not the default: d = 40 N = 4096 515-521 vs 456-478 us, pipeline -2.1 % (same box). On gfx950
+          // v_exp_f32 issues in 8 cycles vs 4 for an FMA (MI355X_MICROARCH constants), so every polynomial exp costs
+          // ~4x the issue time of the transcendental it replaces in this issue-bound loop.
+          const float e = (POLY && !RAGGED && kf == 3) ? exp2_poly(s[f][kf][i]) : __builtin_amdgcn_exp2f(s[f][kf][i]);
           s[f][kf][i] = e;
           if (!SUM_BY_MFMA) ls += e;
         }
@@ -331,7 +354,7 @@ SDMOE_DEV float16v mfma32x32x16(half8 a, half8 b, float16v c) {
 }
 
 template <int D>
-__global__ __launch_bounds__(256, (D <= 40 ? 4 : (D >= 160 ? 1 : 2))) void attn32_kernel(AttnParams p) {
+__global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn32_kernel(AttnParams p) {
   constexpr int NQC = (D + 15) / 16;                  // 16-deep QK contraction steps (d zero-padded to 16 NQC)
   constexpr int DQ = 16 * NQC;
   constexpr bool SUM_MFMA = (D % 32) != 0 && (D % 4) == 0;  // ones column at d = D inside the last O^T block
@@ -341,20 +364,30 @@ __global__ __launch_bounds__(256, (D <= 40 ? 4 : (D >= 160 ? 1 : 2))) void attn3
   constexpr bool ONES_K = (D % 16) == 8;
   constexpr int NDB = (D + (SUM_MFMA ? 1 : 0) + 31) / 32;   // 32-row blocks of O^T
   constexpr int KB = 64;                              // keys per tile
-  constexpr int RS = DQ + 8;                          // K/V row stride (halves): RS/8 odd -> conflict-free K reads
+  constexpr int RS = DQ + 8;                          // K row stride (halves): RS/8 odd -> conflict-free K reads
   static_assert((RS / 8) % 2 == 1, "row stride must be an odd number of 16-B slots");
   constexpr int CH = D / 8;                           // real 16-B chunks per row (the rest load as zeros)
   constexpr int SL = RS / 8;
-  constexpr int TILE = KB * RS;
-  constexpr int NPIECE = TILE * 2 / 1024;             // 1-KiB LDS-DMA wave-instructions per K (or V) tile
-  static_assert(NPIECE * 1024 == TILE * 2, "tile must be whole 1-KiB pieces");
-  constexpr int NPW = (2 * NPIECE + 3) / 4;           // per wave (the last round partly empty)
-  constexpr int TAIL = 64;                            // O^T blocks past RS over-read the last V row (discarded rows)
-  constexpr int VOFF = TILE + TAIL, COFF = VOFF + TILE + TAIL, SLOT = COFF + 8;
+  // V row stride: SLV 16-B slots with SLV = 4 (mod 8), >= the 32 NDB columns the O^T blocks read, so the 8 rows x
+  // 64 B of one V^T transposed read cover all 128 banks once (the K stride, 11 slots at d = 80, gave 3-way
+  // conflicts); the columns past D load as zeros
+  constexpr int SLV = ((4 * NDB + 3) / 8) * 8 + 4;
+  constexpr int RSV = SLV * 8;
+  constexpr int TILE = KB * RS, TILEV = KB * RSV;
+  constexpr int NPK = TILE * 2 / 1024, NPV = TILEV * 2 / 1024;  // 1-KiB LDS-DMA wave-instructions per K / V tile
+  static_assert(NPK * 1024 == TILE * 2 && NPV * 1024 == TILEV * 2, "tiles must be whole 1-KiB pieces");
+  constexpr int NPW = (NPK + NPV + 3) / 4;             // per wave (the last round partly empty)
+  constexpr int TAIL = 64;                            // zeroed tail behind the K tile
+  constexpr int VOFF = TILE + TAIL, SLOT = VOFF + TILEV;
+  static_assert(SLV >= 4 * NDB, "V rows hold every column the O^T blocks read");
   constexpr float RESCALE_THR = 8.0f;
   constexpr unsigned OOB = 0x80000000u;
   __shared__ __attribute__((aligned(1024))) half_t S0[SLOT];
   __shared__ __attribute__((aligned(1024))) half_t S1[SLOT];
+  // the ones column's V^T operand: one [1 0 0 0 | 0 0 0 0] slot per row class r = row mod 8, placed on the banks row r's
+  // slot of column D would occupy in the V tile, so its 8 reader lanes neither share a slot nor collide with the others
+  constexpr int ONES_AT = (VOFF / 8 + D / 8) % 32;    // 16-B unit of row 0's column-D slot, modulo the 512-B bank cycle
+  __shared__ __attribute__((aligned(1024))) half_t ONES[SUM_MFMA ? 256 : 1];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -375,9 +408,10 @@ __global__ __launch_bounds__(256, (D <= 40 ? 4 : (D >= 160 ? 1 : 2))) void attn3
 #pragma unroll
   for (int j = 0; j < NPW; ++j) {
     const int gp = wave + 4 * j;
-    const bool isk = gp < NPIECE;
-    const int pc = isk ? gp : gp - NPIECE;
-    const int slot = pc * 64 + lane, r = slot / SL, c = slot - (slot / SL) * SL;
+    const bool isk = gp < NPK;
+    const int pc = isk ? gp : gp - NPK;
+    const int sl = isk ? SL : SLV;
+    const int slot = pc * 64 + lane, r = slot / sl, c = slot - (slot / sl) * sl;
     const long ld = isk ? p.ldk : p.ldv;
     voff[j] = c < CH ? (unsigned)(r * ld * 2 + c * 16) : OOB;
     vstep[j] = (unsigned)(KB * ld * 2);
@@ -386,13 +420,21 @@ __global__ __launch_bounds__(256, (D <= 40 ? 4 : (D >= 160 ? 1 : 2))) void attn3
   auto issue_tile = [&](half_t* Sd) {
 #pragma unroll
     for (int j = 0; j < NPW; ++j) {
-      if (wave + 4 * j < 2 * NPIECE) bld16(wave + 4 * j < NPIECE ? rsK : rsV, Sd + ldsoff[j], voff[j]);
+      if (wave + 4 * j < NPK + NPV) bld16(wave + 4 * j < NPK ? rsK : rsV, Sd + ldsoff[j], voff[j]);
       voff[j] += vstep[j];
     }
   };
 
-  for (int i = tid; i < TAIL; i += 256) S0[TILE + i] = S1[TILE + i] = S0[VOFF + TILE + i] = S1[VOFF + TILE + i] = 0;
-  if (tid < 8) S0[COFF + tid] = S1[COFF + tid] = (half_t)(tid == 0 ? 1.f : 0.f);
+  for (int i = tid; i < TAIL; i += 256) S0[TILE + i] = S1[TILE + i] = 0;
+  if constexpr (SUM_MFMA) {
+    for (int i = tid; i < 256; i += 256) {
+      const int u = i / 8;  // 16-B unit; row class r sits at unit (ONES_AT + SLV r) mod 32
+      bool one = false;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) one |= (i % 8 == 0) && u == (ONES_AT + SLV * r) % 32;
+      ONES[i] = (half_t)(one ? 1.f : 0.f);
+    }
+  }
 
   const int nkt = (p.Nk + KB - 1) / KB;
   issue_tile(S0);
@@ -426,7 +468,8 @@ __global__ __launch_bounds__(256, (D <= 40 ? 4 : (D >= 160 ? 1 : 2))) void attn3
   // V^T operand addresses: lane (group g16 = lane / 16, index 4 tq + tp in it) supplies row 4 hf + tq (+ 8 for the
   // second read) and columns 16 (g16 & 1) + 4 tp of its 4 x 16 transposed-read block
   const int gi = lane & 15, g16 = lane >> 4, tq = gi >> 2, tp = gi & 3;
-  const int vbase = VOFF + (4 * hf + tq) * RS + 16 * (g16 & 1) + 4 * tp;
+  const int vbase = VOFF + (4 * hf + tq) * RSV + 16 * (g16 & 1) + 4 * tp;
+  const half_t* ones_at = ONES + 8 * ((ONES_AT + SLV * (4 * hf + tq)) % 32);  // rows 4 hf + tq (+ 8): same class
   const bool onecol = SUM_MFMA && (g16 & 1) == (D % 32) / 16 && tp == (D % 16) / 4;
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -506,9 +549,9 @@ __global__ __launch_bounds__(256, (D <= 40 ? 4 : (D >= 160 ? 1 : 2))) void attn3
       for (int cs = 0; cs < 2; ++cs)
 #pragma unroll
         for (int db = 0; db < NDB; ++db) {
-          const half_t* a1 = St + vbase + (32 * kb + 16 * cs) * RS + 32 * db;
-          const half_t* a2 = a1 + 8 * RS;
-          if (SUM_MFMA && db == NDB - 1 && onecol) a1 = a2 = St + COFF;
+          const half_t* a1 = St + vbase + (32 * kb + 16 * cs) * RSV + 32 * db;
+          const half_t* a2 = a1 + 8 * RSV;
+          if (SUM_MFMA && db == NDB - 1 && onecol) a1 = a2 = ones_at;
           const half4 lo = ds_read_tr(a1), hi = ds_read_tr(a2);
           const half8 a = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
           oacc[db] = mfma32x32x16(a, pb[kb][cs], oacc[db]);
@@ -600,6 +643,9 @@ int launch(const AttnParams& p, int nimg, hipStream_t s) {
   } else if (use8 && D <= 80) {
     dim3 grid((p.Nq + 255) / 256, p.heads, nimg);
     attn_fwd_kernel<D, 2, (D <= 80 ? 8 : 4)><<<grid, (D <= 80 ? 512 : 256), 0, s>>>(p);
+  } else if (g_attn_nqf == 40 && D == 40) {
+    dim3 grid((p.Nq + 255) / 256, p.heads, nimg);
+    attn_fwd_kernel<D, 2, 8, (D == 40 ? 1 : 0)><<<grid, 512, 0, s>>>(p);
   } else if (g_attn_nqf == 16 && D <= 40) {
     dim3 grid((p.Nq + 511) / 512, p.heads, nimg);
     attn_fwd_kernel<D, 2, (D <= 40 ? 16 : 4)><<<grid, (D <= 40 ? 1024 : 256), 0, s>>>(p);
@@ -614,7 +660,7 @@ int launch(const AttnParams& p, int nimg, hipStream_t s) {
 }  // namespace
 
 int sdmoe_attn_set_nqf(int v) {
-  if (v != 0 && v != 1 && v != 2 && v != 4 && v != 8 && v != 16) return SDMOE_EARG;
+  if (v != 0 && v != 1 && v != 2 && v != 4 && v != 8 && v != 16 && v != 40) return SDMOE_EARG;
   g_attn_nqf = v;
   return SDMOE_OK;
 }

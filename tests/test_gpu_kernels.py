@@ -264,7 +264,7 @@ def test_attention(d, Nq, Nk):
     close(out, ref)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 4, 8, 16])
+@pytest.mark.parametrize("variant", [1, 2, 4, 8, 16, 40])
 @pytest.mark.parametrize("d,Nq,Nk", [(40, 256, 256), (40, 300, 77), (80, 200, 200), (64, 300, 300),
                                      (32, 130, 130)])
 def test_attention_forced_variant(variant, d, Nq, Nk):

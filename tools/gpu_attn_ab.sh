@@ -10,7 +10,7 @@ timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 tail -1 $O/tests.log
 SDMOE_LIB=$P timeout -k 10 300 python tools/micro_ab.py attn > $O/micro_prev.log 2>&1 || { tail -20 $O/micro_prev.log; exit 1; }
 echo "== previous library"; grep -v amdgpu.ids $O/micro_prev.log
-timeout -k 10 300 python tools/micro_ab.py attn --tune "" --tune "4=8" --tune "4=16" > $O/micro.log 2>&1 || { tail -20 $O/micro.log; exit 1; }
+timeout -k 10 300 python tools/micro_ab.py attn --tune "" ${MICRO_TUNES:---tune 4=8 --tune 4=16} > $O/micro.log 2>&1 || { tail -20 $O/micro.log; exit 1; }
 echo "== current"; grep -v amdgpu.ids $O/micro.log
 BA="--steps 4 --warmup 1 --no-cpu-baseline --e2e-steps 0 --no-roofline"
 for i in 1 2 3; do

@@ -1,5 +1,5 @@
 """Run one kernel shape repeatedly (for rocprofv3 --pmc passes).
-usage: python tools/kernel_micro.py attn|conv|linear|geglu [--iters 20] [--diag BITS]"""
+usage: python tools/kernel_micro.py attn|conv|linear|geglu [--iters 20] [--diag BITS] [--d 40] [--tune k=v,...]"""
 import argparse
 import os
 import sys
@@ -18,12 +18,17 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--nimg", type=int, default=16)
     ap.add_argument("--diag", type=int, default=0, help="GEMM diagnostics bits (sdmoe_tune knob 6)")
+    ap.add_argument("--d", type=int, default=40, help="attn: head dim (8 heads, N = 4096)")
+    ap.add_argument("--tune", default="", help="extra sdmoe_tune settings 'knob=value,...'")
     a = ap.parse_args()
     from sdmoe import _lib
     _lib.check(_lib.load().sdmoe_tune(6, a.diag), "tune")
+    for kv in filter(None, a.tune.split(",")):
+        k, v = kv.split("=")
+        _lib.check(_lib.load().sdmoe_tune(int(k), int(v)), "tune")
     n, dev = a.nimg, "cuda"
     if a.what == "attn":
-        C = 320
+        C = 8 * a.d
         q = torch.randn(n * 4096, 3 * C, device=dev).half()
         f = lambda: ops.attention(q[:, :C], q[:, C:2 * C], q[:, 2 * C:], n, 4096, 4096, 8)  # noqa: E731
     elif a.what == "conv":
