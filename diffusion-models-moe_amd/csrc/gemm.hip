@@ -1329,6 +1329,7 @@ extern "C" int sdmoe_mask_weight(const void* W, const void* bits, long N, long K
 
 int sdmoe_attn_set_nqf(int v);  // attention.hip
 int sdmoe_gn_set_fused(int v);  // norm.hip
+extern int g_topk_tpw;          // moe.hip
 
 extern "C" int sdmoe_tune(int knob, int value) {
   if (knob == 4) return sdmoe_attn_set_nqf(value);
@@ -1341,5 +1342,6 @@ extern "C" int sdmoe_tune(int knob, int value) {
   if (knob == 3 && (value == 0 || value == 1)) { g_prio = value; return SDMOE_OK; }
   if (knob == 6 && value >= 0 && value <= 15) { g_diag = value; return SDMOE_OK; }
   if (knob == 8 && (value == 0 || value == 1)) { g_res16 = value; return SDMOE_OK; }
+  if (knob == 15 && (value == 0 || value == 1 || value == 4)) { g_topk_tpw = value; return SDMOE_OK; }
   return SDMOE_EARG;
 }

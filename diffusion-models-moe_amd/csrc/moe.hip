@@ -156,12 +156,14 @@ struct Slots64 {  // per-slot 64-bit expert masks (slot i = experts 64 i .. 64 i
   SDMOE_DEV unsigned long long get(int i) const { return i == 0 ? a : (i == 1 ? b : (i == 2 ? c : d)); }
 };
 
-template <int SLOTS, int SC, bool KEEPOUT>  // SC: compile-time expert size (0 = runtime S)
-__global__ __launch_bounds__(256) void moe_topk_mask_kernel(
+// TPW tokens per wave (4, or 1 for M <= 16384: the per-token radix search is a serial ballot / popcount chain, and
+// with 4 tokens per wave the 4096-token launches ran 256 workgroups -- one wave per SIMD, 18.7 us at E = 256);
+// always 16 tokens per workgroup (4 or 16 waves)
+template <int SLOTS, int SC, bool KEEPOUT, int TPW>  // SC: compile-time expert size (0 = runtime S)
+__global__ __launch_bounds__(64 * 16 / TPW) void moe_topk_mask_kernel(
     half_t* __restrict__ P, long ldp, int M, int F, int E, int S_, int k, const half_t* __restrict__ score, long lds,
     const uint32_t* __restrict__ removed, uint32_t* __restrict__ sel_out, unsigned long long* __restrict__ keep) {
-  constexpr int TPW = 4;                        // tokens per wave
-  constexpr int WPB = 4;                        // waves per workgroup
+  constexpr int WPB = 16 / TPW;                 // waves per workgroup
   constexpr int TPB = TPW * WPB;                // tokens per workgroup
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int S = SC ? SC : S_;
@@ -172,16 +174,18 @@ __global__ __launch_bounds__(256) void moe_topk_mask_kernel(
   // indices: a per-lane validity branch around each load made the compiler wait for each separately), then the
   // removed bits; separate row arrays keep every index constant
   half_t sc0[SLOTS], sc1[SLOTS], sc2[SLOTS], sc3[SLOTS];
-  static_assert(TPW == 4, "four score rows per wave");
+  static_assert(TPW == 4 || TPW == 1, "one or four score rows per wave");
   auto load_row = [&](half_t (&dst)[SLOTS], int t) {
     const half_t* srow = score + (long)min(mw + t, M - 1) * lds;
 #pragma unroll
     for (int i = 0; i < SLOTS; ++i) dst[i] = srow[min(lane + 64 * i, E - 1)];
   };
   load_row(sc0, 0);
-  load_row(sc1, 1);
-  load_row(sc2, 2);
-  load_row(sc3, 3);
+  if constexpr (TPW == 4) {
+    load_row(sc1, 1);
+    load_row(sc2, 2);
+    load_row(sc3, 3);
+  }
   uint32_t rmw[SLOTS];  // removed bits of this lane's experts
   bool valid[SLOTS];
 #pragma unroll
@@ -269,9 +273,11 @@ __global__ __launch_bounds__(256) void moe_topk_mask_kernel(
     }
   };
   process(sc0, 0);
-  process(sc1, 1);
-  process(sc2, 2);
-  process(sc3, 3);
+  if constexpr (TPW == 4) {
+    process(sc1, 1);
+    process(sc2, 2);
+    process(sc3, 3);
+  }
   if constexpr (KEEPOUT) {
     __syncthreads();
     const int m0 = blockIdx.x * TPB, nks = F >> 6;
@@ -284,14 +290,21 @@ __global__ __launch_bounds__(256) void moe_topk_mask_kernel(
 
 }  // namespace
 
+int g_topk_tpw = 0;  // sdmoe_tune knob 15: 0 = by M (default), 1 / 4 = always 1 / 4 tokens per wave
+
 template <bool KEEPOUT>
 int launch_topk(half_t* P, long ldp, int M, int F, int E, int esize, int k, const half_t* sc, long ld_score,
                 const uint32_t* rm, uint32_t* sel_out, unsigned long long* keep, hipStream_t s) {
-  const int blocks = (M + 15) / 16;  // 4 waves x 4 tokens per workgroup
+  const int blocks = (M + 15) / 16;  // 16 tokens per workgroup: 4 waves x 4 tokens, or 16 waves x 1 (M <= 16384)
   const size_t lds = KEEPOUT ? (size_t)16 * ((F >> 6) + 1) * 8 : 0;
-#define SDMOE_TOPK_MASK(SL, SC) \
-  moe_topk_mask_kernel<SL, SC, KEEPOUT><<<blocks, 256, lds, s>>>(P, ldp, M, F, E, esize, k, sc, ld_score, rm, \
-                                                                   sel_out, keep)
+  const bool one = g_topk_tpw == 1 || (M <= 16384 && g_topk_tpw != 4);
+#define SDMOE_TOPK_MASK(SL, SC)                                                                                 \
+  if (one)                                                                                                      \
+    moe_topk_mask_kernel<SL, SC, KEEPOUT, 1><<<blocks, 1024, lds, s>>>(P, ldp, M, F, E, esize, k, sc, ld_score, \
+                                                                       rm, sel_out, keep);                      \
+  else                                                                                                          \
+    moe_topk_mask_kernel<SL, SC, KEEPOUT, 4><<<blocks, 256, lds, s>>>(P, ldp, M, F, E, esize, k, sc, ld_score,  \
+                                                                      rm, sel_out, keep)
   if (esize == 20) {  // the reference's expert size (KMeansConstrained, 20 neurons): divisions by a constant
     if (E <= 64) SDMOE_TOPK_MASK(1, 20);
     else if (E <= 128) SDMOE_TOPK_MASK(2, 20);

@@ -342,7 +342,9 @@ int sdmoe_cfg_multistep_step(const void* eps, long lde, float* lat, int B, int H
    knob 7 = sdmoe_groupnorm at HW <= 256: 1 (default) statistics + apply in one launch with the rows held in
    registers, 2 the same launch re-reading the rows for the apply, 0 two launches;
    knob 8 = GEMM residual epilogue: 1 (default) output rounded to fp16 then the residual added in fp16 arithmetic
-   (diffusers' fp16 `linear(x) + residual`), 0 = accumulator + residual rounded once (fp32 staging). */
+   (diffusers' fp16 `linear(x) + residual`), 0 = accumulator + residual rounded once (fp32 staging);
+   knob 15 = top-k expert selection kernels: 0 (default) one token per wave at M <= 16384, four above; 1 / 4 = always
+   one / four tokens per wave. */
 int sdmoe_tune(int knob, int value);
 
 /* out = a + b (fp16, n % 8 == 0). */

@@ -273,6 +273,36 @@ def test_keep_mask_in_down_projection_bit_exact(M, C, E, k, nrem, N):
     assert torch.equal(y, y_ref)
 
 
+@pytest.mark.parametrize("M,E,k,nrem", [(4096, 256, 51, 20), (1000, 64, 12, 5), (16384, 128, 25, 0), (16385, 128, 25, 3)])
+def test_topk_one_token_per_wave_matches_four(M, E, k, nrem):
+    """The top-k kernels at one token per wave (M <= 16384, default) and four per wave (sdmoe_tune knob 15 = 4):
+    identical selection, masked product and keep bits, on scores quantised to force ties at the k-th place."""
+    from sdmoe import _lib
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(M + E)
+    esize = 20
+    F = E * esize
+    routing = ops.Routing(torch.arange(F) // esize, E, k, DEV)
+    score = (torch.randint(0, 12, (M, E), generator=g).float() / 4).half().to(DEV)  # many exact ties
+    P = torch.randn(M, F, generator=g).half().to(DEV)
+    removed = ops.removed_bits(torch.randperm(E, generator=g)[:nrem].tolist(), E, DEV) if nrem else None
+    res = {}
+    for tpw in (0, 4):
+        _lib.check(lib.sdmoe_tune(15, tpw), "tune")
+        try:
+            Pm = P.clone()
+            sel_m = torch.zeros((M, (E + 31) // 32), dtype=torch.int32, device=DEV)
+            sel_k = torch.zeros_like(sel_m)
+            ops.moe_topk_mask(Pm, score, routing, removed=removed, sel_out=sel_m)
+            keep = ops.moe_topk_keep(score, routing, M, removed=removed, sel_out=sel_k)
+            res[tpw] = (Pm, sel_m, sel_k, keep)
+        finally:
+            _lib.check(lib.sdmoe_tune(15, 0), "tune")
+    for a_, b_ in zip(res[0], res[4]):
+        assert torch.equal(a_, b_)
+    assert torch.equal(res[0][1], res[0][2])
+
+
 def test_fused_geglu_dense_matches_unfused():
     M, C = 1500, 320
     g = torch.Generator().manual_seed(7)

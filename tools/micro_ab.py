@@ -1,7 +1,7 @@
 """Per-launch device time of U-Net ops at the bench's shapes (16 images), under one or more sdmoe_tune settings.
 
 usage: python tools/micro_ab.py FAMILY [--tune "k=v,k=v"]... [--iters 50]
-FAMILY: gn | linear | geglu | conv | attn | all. Each case is launched back to back `iters` times between two HIP events on
+FAMILY: gn | linear | geglu | conv | attn | topk | all. Each case is launched back to back `iters` times between two HIP events on
 the launch stream (warm L2: a relative A/B tool, not the pipeline's cold-cache numbers: tools/op_breakdown.py)."""
 import argparse
 import os
@@ -94,6 +94,17 @@ def attn_cases():
     return out
 
 
+def topk_cases():
+    """Top-k expert selection (keep bits for the down projection) at the U-Net levels' token counts."""
+    out = []
+    for M, E in [(65536, 64), (16384, 128), (4096, 256), (1024, 256)]:
+        routing = ops.Routing(torch.arange(20 * E) // 20, E, E // 5, DEV)
+        score = rnd(M, E)
+        out.append((f"topk_keep M={M} E={E}", lambda score=score, r=routing, M=M: ops.moe_topk_keep(score, r, M),
+                    M * E * 2 + M * 20 * E // 8, "B"))
+    return out
+
+
 def run(cases, iters):
     res = {}
     for name, f, work, unit in cases:
@@ -119,7 +130,8 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     a = ap.parse_args()
     lib = _lib.load()
-    fam = {"gn": gn_cases, "linear": linear_cases, "geglu": geglu_cases, "conv": conv_cases, "attn": attn_cases}
+    fam = {"gn": gn_cases, "linear": linear_cases, "geglu": geglu_cases, "conv": conv_cases, "attn": attn_cases,
+           "topk": topk_cases}
     cases = [c for k in (fam if a.family == "all" else [a.family]) for c in fam[k]()]
     settings = a.tune or [""]
     table = {}
@@ -131,7 +143,7 @@ def main():
             r = run(cases, a.iters)
             for kv in filter(None, st.split(",")):  # back to defaults (0) unless the knob's default differs
                 k, _ = kv.split("=")
-                _lib.check(lib.sdmoe_tune(int(k), 1 if k in ("7", "8") else 0), "tune")
+                _lib.check(lib.sdmoe_tune(int(k), 1 if k in ("7", "8", "14") else 0), "tune")
             for name, v in r.items():
                 table.setdefault(name, {}).setdefault(st, []).append(v)
     for name, per in table.items():
