@@ -160,6 +160,18 @@ constexpr int KEEP_LUT_BYTES = 16 * 8;  // 4 keep bits -> 4 x 16-bit lane masks
 // Routed-GEGLU expert scores over one staged pass of a wave's tile: the activated gates (fp16) of RG rows x NH
 // neurons, experts = contiguous S-neuron slices (neurons pre-permuted expert-major). score = fp32 sum in neuron order,
 // rounded to fp16 (as sdmoe_geglu_route). Row-fastest lane mapping (lane -> row id % RG).
+// acc + (float)h for the low / high fp16 half of x in ONE v_fma_mix_f32 (fma(h, 1.0, acc): the f16 -> f32 conversion
+// is exact and the fma rounds once, so the result is bit-identical to cvt + add; the compiler folds fma(h, 1, acc)
+// back into the two-instruction cvt + add)
+SDMOE_DEV float add_f16_lo(float acc, unsigned x) {
+  asm("v_fma_mix_f32 %0, %1, 1.0, %0 op_sel_hi:[1,0,0]" : "+v"(acc) : "v"(x));
+  return acc;
+}
+SDMOE_DEV float add_f16_hi(float acc, unsigned x) {
+  asm("v_fma_mix_f32 %0, %1, 1.0, %0 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(acc) : "v"(x));
+  return acc;
+}
+
 template <int S, int NH, int RG>
 SDMOE_DEV void expert_sums(const GemmParams& p, const half_t* sg, int mrow0, int n0, int lane) {
   constexpr int NE = NH / S;
@@ -168,12 +180,13 @@ SDMOE_DEV void expert_sums(const GemmParams& p, const half_t* sg, int mrow0, int
     const int m = mrow0 + r;
     const half_t* rp = sg + r * NH + e * S;
     float acc = 0.f;
-    if constexpr (S % 4 == 0) {  // 8-B aligned quads
+    if constexpr (S % 4 == 0) {  // 8-B aligned quads, summed in neuron order by mixed-precision fmas
 #pragma unroll
       for (int q = 0; q < S / 4; ++q) {
-        const half4 x = *reinterpret_cast<const half4*>(rp + 4 * q);
-#pragma unroll
-        for (int t = 0; t < 4; ++t) acc += (float)x[t];
+        typedef unsigned u2 __attribute__((ext_vector_type(2)));
+        const u2 x = *reinterpret_cast<const u2*>(rp + 4 * q);
+        acc = add_f16_hi(add_f16_lo(acc, x[0]), x[0]);
+        acc = add_f16_hi(add_f16_lo(acc, x[1]), x[1]);
       }
     } else {
 #pragma unroll
@@ -704,6 +717,9 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int nsel = (fg & 1) * 4 + (fg >> 1) * 2;
+    constexpr int CPO = NH / 8, RPI = 64 / CPO;  // copy-out: 16-B chunks per staged row, rows per 64-lane round
+    const int lr = lane / CPO, lc = lane - (lane / CPO) * CPO;
+    half_t* const cout = p.C + (long)(mw + lr) * p.ldc + nw / 2 + 8 * lc;
     // this lane's bias pairs in every fragment (value cols 16 j + nsel, +1; gate cols +8), hoisted out of the rows
     float2v bvv[FN], bgg[FN];
 #pragma unroll
@@ -751,12 +767,16 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       const int mr0 = mw + h * RG;
-      for (int id = lane; id < RG * (NH / 8); id += 64) {
-        const int r = id / (NH / 8), c = id - r * (NH / 8);
-        const int m = mr0 + r;
-        const half8 o = *reinterpret_cast<const half8*>(sp + r * NH + 8 * c);
-        if (p.diag & 8) asm volatile("" ::"v"(o));
-        else if (m < p.M) *reinterpret_cast<half8*>(p.C + (long)m * p.ldc + nw / 2 + 8 * c) = o;
+      // copy-out: lane -> (row lr + RPI it, 16-B chunk lc) with a fixed per-lane chunk, so the global address is the
+      // hoisted per-lane pointer plus a uniform row offset (no per-chunk 64-bit index arithmetic)
+#pragma unroll
+      for (int it = 0; it < (RG + RPI - 1) / RPI; ++it) {
+        const int r = it * RPI + lr;
+        if (lr < RPI && r < RG) {
+          const half8 o = *reinterpret_cast<const half8*>(sp + r * NH + 8 * lc);
+          if (p.diag & 8) asm volatile("" ::"v"(o));
+          else if (mr0 + r < p.M) *reinterpret_cast<half8*>(cout + (long)(h * RG + it * RPI) * p.ldc) = o;
+        }
       }
       if (p.score) {
         switch (p.esize) {
