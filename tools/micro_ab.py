@@ -78,7 +78,7 @@ def conv_cases():
 
 def attn_cases():
     out = []
-    for N, C, heads in [(4096, 320, 8), (1024, 640, 8), (256, 1280, 8), (64, 1280, 8)]:
+    for N, C, heads in [(4096, 320, 8), (1024, 640, 8), (256, 1280, 8), (64, 1280, 8), (4096, 640, 10), (1024, 1280, 20)]:
         q = rnd(N_IMG * N, 3 * C)
         d = C // heads
         out.append((f"attn N={N} d={d}", lambda q=q, C=C, N=N, heads=heads:
