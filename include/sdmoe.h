@@ -337,7 +337,9 @@ int sdmoe_cfg_multistep_step(const void* eps, long lde, float* lat, int B, int H
    workgroups share weight slices in its L2), 0 split fastest; knob 2 = K-step
    depth (0 auto, 32, 64); knob 3 = MFMA-cluster wave priority (0/1); knob 4 = attention kernel (0 auto by shape,
    1 = 32x32x16 MFMA kernel, 2 / 4 = 4-wave 16x16x32 kernel with 32 / 64 queries per wave, 64 for head_dim <= 40
-   only; 8 = 16x16x32 kernel in 8-wave workgroups (head_dim <= 80), 16 = in 16-wave workgroups (head_dim <= 40));
+   only; 8 = 16x16x32 kernel in 8-wave workgroups (head_dim <= 80), 16 = in 16-wave workgroups (head_dim <= 40);
+   40 = the 8-wave kernel with a quarter of the exp2s as a polynomial on the FMA pipe (head_dim 40; evaluation only,
+   measured slower));
    knob 6 = GEMM diagnostics bits (1 no K-loop loads, 2 no MFMA, 4 no epilogue, 8 no global stores);
    knob 7 = sdmoe_groupnorm at HW <= 256: 1 (default) statistics + apply in one launch with the rows held in
    registers, 2 the same launch re-reading the rows for the apply, 0 two launches;
