@@ -46,6 +46,10 @@ def parse():
                    help="ddim: the metric (50 U-Net calls); pndm: the reference's default (51 calls)")
     p.add_argument("--mask", choices=["remove", "union", "none"], default="remove")
     p.add_argument("--topk", type=float, default=0.2)
+    p.add_argument("--act", choices=["relu", "gelu"], default=None,
+                   help="FFN gate activation: relu = the relufied U-Net (find_and_change_geglu; default for sd14, the "
+                        "reference's fine-tuned relufied SD, utils.py:66-74); gelu = the model's own GELU (default for "
+                        "sdxl: the reference loads SDXL-base without relufying it, utils.py:111-112)")
     p.add_argument("--topk-mask", choices=["down", "pass"], default="down",
                    help="down: the top-k mask is applied by the down projection as it reads the GEGLU product "
                         "(sdmoe_linear_keep); pass: a separate masking pass over the product (A/B reference)")
@@ -145,7 +149,8 @@ def build(args, world, rank, dev):
         pipe.output_type = "pt" if on else "latent"
     if e2e is not None:
         set_e2e(args.decode)
-    find_and_change_geglu(pipe.unet)                  # relufied U-Net (config 2/3)
+    if args.act == "relu":
+        find_and_change_geglu(pipe.unet)              # relufied U-Net (configs 2-4); SDXL keeps its GELU (config 5)
     moefy_synthetic(pipe, args.topk, 20, seed=0)      # E = 4C/20 experts, k = int(E*topk)
     geglus = [m for n, m in pipe.unet.named_modules() if n.endswith("ff.net.0")]
     T = args.inference_steps + (1 if args.scheduler == "pndm" else 0)  # U-Net calls = counter timesteps
@@ -346,6 +351,8 @@ def main():
         return launch_probe(args)
     if args.batch is None:
         args.batch = 2 if args.model == "sdxl" else 8
+    if args.act is None:
+        args.act = "gelu" if args.model == "sdxl" else "relu"
     world, rank, local = setup_dist(args.gpus)
     dev = f"cuda:{local}" if world > 1 else "cuda:0"
     from sdmoe import ops, _lib
@@ -449,7 +456,7 @@ def main():
             "value": round(value, 4), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp16", "data": "synthetic",
-            "config": {"workload": f"{'SDXL-base' if args.model == 'sdxl' else 'SD-1.4'} MoE-fied (relu, top-k {args.topk}, expert 20) + "
+            "config": {"workload": f"{'SDXL-base' if args.model == 'sdxl' else 'SD-1.4'} MoE-fied ({args.act}, top-k {args.topk}, expert 20) + "
                                    f"{'RemoveExperts skilled-expert mask' if args.mask != 'none' else 'no mask'}"
                                    f"{' + union Wanda mask' if args.mask == 'union' else ''}, "
                                    f"{8 * cfg.sample_size}^2 (4x{cfg.sample_size}x{cfg.sample_size} latents), "

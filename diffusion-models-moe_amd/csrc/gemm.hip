@@ -126,8 +126,15 @@ SDMOE_DEV void epilogue8(const GemmParams& p, int m, int n, float (&v)[8]) {
   }
   if (p.R) {
     half8 rr = *reinterpret_cast<const half8*>(p.R + (long)m * p.ldr + n);
+    if (p.res16 && p.act == ACT_NONE) {
+      // the fp16 staging path's order (knob 8): output rounded to fp16, residual added, rounded again -- so split-K
+      // launches (this reduce) and unsplit ones give the same residual semantics for every shape
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] += (float)rr[j];
+      for (int j = 0; j < 8; ++j) v[j] = (float)(half_t)v[j] + (float)rr[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += (float)rr[j];
+    }
   }
   half8 o;
 #pragma unroll

@@ -313,8 +313,10 @@ __global__ __launch_bounds__(256) void gn_fused_reg_kernel(const half_t* __restr
 #pragma unroll
   for (int i = 0; i < 8; ++i) { red[tid][i] = s1[i]; red[tid][8 + i] = s2[i]; }
   __syncthreads();
-  if (tid < nq * 16) {  // (chunk c, value i): the R row phases in order, as gn_small_kernel's per-c loop
-    const int c = tid >> 4, i = tid & 15;
+  // (chunk c, value i): the R row phases in order, as gn_small_kernel's per-c loop; nq * 16 can exceed the 256
+  // threads (WC up to 256 -> nq up to 32, e.g. C = 576 / 1152 / 1600 with 32 groups), hence the stride
+  for (int id = tid; id < nq * 16; id += 256) {
+    const int c = id >> 4, i = id & 15;
     float a = 0.f;
     for (int p = 0; p < R; ++p) a += red[p * nq + c][i];
     csum[i >> 3][c * 8 + (i & 7)] = a;

@@ -112,7 +112,10 @@ class WandaRemoveNeuronsFast(NeuronPredictivity):
         version, perm) with sdmoe_mask_weight and kept in HBM; None when it would exceed bake_budget_bytes (shared by
         all receivers of the process on that device). The entry keeps references to the weight and perm it was made
         from (so neither address can be recycled while it lives) and is replaced -- its HBM released -- when either
-        changes for the same (t, l)."""
+        changes for the same (t, l).
+        `weight` must share the module parameter's version counter (the Parameter itself or `.detach()`, never
+        `.data`, whose counter is a fresh 0): an in-place update (load_state_dict / copy_ / a LoRA merge) keeps the
+        address but bumps the version, and the stale bake is then replaced."""
         key = ("baked", t, l, perm is None)
         ent = self._dev.get(key)
         if ent is not None and ent[0].data_ptr() == weight.data_ptr() and ent[1] == weight._version \
@@ -143,7 +146,7 @@ class WandaRemoveNeuronsFast(NeuronPredictivity):
         ff.net.2's weight with its columns in that order. Returns y + residual; advances the (t, l) counter."""
         bits = self.device_bits(self.timestep, self.layer, module.weight.device)
         self._check_shape(bits, module.weight, "ff.net.2")
-        wb = self.baked_weight(self.timestep, self.layer, module.weight.data, perm)
+        wb = self.baked_weight(self.timestep, self.layer, module.weight.detach(), perm)
         if wb is not None:
             y = ops.linear_masked(x2d, wb, module.bias, keep=keep, residual=residual)
         else:
@@ -178,7 +181,7 @@ class WandaRemoveNeuronsFast(NeuronPredictivity):
         x = input[0]
         bits = self.device_bits(self.timestep, self.layer, module.weight.device)
         self._check_shape(bits, module.weight, "ff.net.2")
-        wb = self.baked_weight(self.timestep, self.layer, module.weight.data)
+        wb = self.baked_weight(self.timestep, self.layer, module.weight.detach())
         if wb is not None:
             y = module.run(x.reshape(-1, x.shape[-1]), weight=wb)
         else:

@@ -542,7 +542,10 @@ def test_groupnorm_small_bench_shapes(H, C):
 @pytest.mark.parametrize("HW,C,nimg,silu", [(1024, 640, 16, True), (1024, 320, 16, False), (1024, 1920, 16, True),
                                             (256, 1280, 16, True), (256, 2560, 16, True), (256, 640, 5, False),
                                             (64, 1280, 16, True), (64, 2560, 16, True), (64, 1280, 3, False),
-                                            (16, 128, 2, True), (1024, 960, 2, True)])
+                                            (16, 128, 2, True), (1024, 960, 2, True),
+                                            # chunk widths with nq = WC/8 > 16 (rows 16.. of the
+                                            # per-chunk reduction were skipped)
+                                            (64, 576, 3, True), (64, 1152, 2, True), (16, 1600, 2, False)])
 def test_groupnorm_single_launch_bit_identical(HW, C, nimg, silu):
     """The single-launch kernels (statistics + apply, HW <= 256: gn_fused_reg_kernel, knob 7 = 1, and
     gn_fused_kernel, knob 7 = 2) vs the two-launch path (gn_small_kernel + gn_apply_kernel, knob 7 = 0): the same

@@ -17,11 +17,13 @@
    256) in tests/test_gpu_sdxl.py.
 2. The full 50-step trajectory: one prompt at 64x64, all 50 DDIM steps (so the t = 20 removal cut-off is crossed),
    vs the fp32 oracle pipeline with the reference hook (fp16 projection, the device's selection teacher-forced).
-   Final latents must agree to max-abs <= 2e-2 x max(1, max|ref|) and PSNR >= 40 dB (the synthetic
-   weights drive |latent| to ~70). Both latents are then decoded to 512^2 RGB, the device's through the HIP VAE and
-   the oracle's through the oracle VAE: pixel tolerance max-abs <= 2e-2 (on [0, 1]) and PSNR >= 40 dB.
-3. Config 4 at its real per-GPU shard: the union Wanda mask + MoE routing at 64x64 latents, 2 prompts, 2 steps,
-   with the same-input selection check of 1 and the trunk vs the oracle.
+   Final latents must agree to rel-L2 <= 3e-3, PSNR >= 65 dB and max-abs <= 3e-3 x max(1, max|ref|) (the measured
+   envelope with ~2-3x margin; the synthetic weights drive |latent| to ~70). Both latents are then decoded to 512^2
+   RGB, the device's through the HIP VAE and the oracle's through the oracle VAE: pixel tolerance max-abs <= 1e-2
+   (on [0, 1]) and PSNR >= 60 dB.
+3. Config 4 at its real per-GPU shard: the union Wanda mask + MoE routing at 64x64 latents, 8 prompts (U-Net
+   batch 16, the bench's shard), 2 steps, with the same-input selection check of 1 on all 16 images and the trunk vs
+   the oracle on 2 of the prompts (each prompt's trajectory is independent of the others in the batch).
 """
 import numpy as np
 import pytest
@@ -66,9 +68,11 @@ def same_input_recorder(cls):
     return Rec
 
 
-def check_same_input(records, mods, lists, act, min_compared=0.95, report=None):
+def check_same_input(records, mods, lists, act, min_compared=0.95, report=None, max_flip_frac=1e-4):
     """Re-run the reference hook (fp16 CPU) on each recorded input; see the module docstring for the contract.
-    Returns the counts (asserting the contract as it goes)."""
+    Returns the counts (asserting the contract as it goes). Near-tie flips (rows within 2 fp16 ulps at the k-th score
+    whose device scores differ from the reference's) are bounded: at most max_flip_frac of all rows (measured: 6 of
+    862,208 at the SD-1.4 batch-16 workload, 2 of 204,800 for SDXL 1024^2, 1 of 215,552 for the union)."""
     tot = dict(rows=0, compared=0, clear=0, exact_tie=0, tie_consistent=0, near_tie=0, near_tie_equal_scores=0,
                near_tie_flips=0, score_bit_equal_rows=0, calls=0)
     weights = {}
@@ -124,6 +128,7 @@ def check_same_input(records, mods, lists, act, min_compared=0.95, report=None):
     if report is not None:
         report(**tot)
     assert tot["compared"] >= min_compared * tot["rows"], tot
+    assert tot["near_tie_flips"] <= max_flip_frac * tot["rows"], tot
     return tot
 
 
@@ -247,18 +252,27 @@ def test_trajectory_50_steps_sd14_64x64(parity_report):
                   latent_psnr_db=p_lat, latent_rel_l2=rel_l2(got, exp), pixel_max_abs=perr, pixel_psnr_db=p_pix,
                   latent_absmax=exp.abs().max().item())
     assert torch.isfinite(got).all()
-    # latents: SURVEY §8d's max-abs 2e-2 relative to the latents' scale (these synthetic-weight trajectories reach
-    # |x| ~ 70, where one fp16 ulp of the eps the U-Net returns is already 3e-2 x 7.5 CFG), and PSNR >= 40 dB
+    # latents, bounded at ~2-3x the measured envelope (round 3: rel-L2 1.08e-3, PSNR 77.5 dB, max-abs 0.075 on
+    # |x| <= 66.6): rel-L2 <= 3e-3, PSNR >= 65 dB, max-abs <= 3e-3 of the latents' scale (SURVEY §8d's 2e-2 max-abs
+    # is absolute for unit-scale latents; these synthetic-weight trajectories reach |x| ~ 70, where one fp16 ulp
+    # of the eps the U-Net returns is already 3e-2 x 7.5 CFG)
     scale = max(1.0, exp.abs().max().item())
-    assert err <= 2e-2 * scale and p_lat >= 40.0, (err, scale, p_lat)
-    # pixels in [0, 1]: absolute max-abs 2e-2 and PSNR >= 40 dB
-    assert perr <= 2e-2 and p_pix >= 40.0, (perr, p_pix)
+    assert rel_l2(got, exp) <= 3e-3 and p_lat >= 65.0 and err <= 3e-3 * scale, (rel_l2(got, exp), p_lat, err, scale)
+    # pixels in [0, 1] (measured: max-abs 3.0e-3, PSNR 66.6 dB): max-abs <= 1e-2, PSNR >= 60 dB
+    assert perr <= 1e-2 and p_pix >= 60.0, (perr, p_pix)
+
+
+def image_rows(sel, nimg, imgs):
+    """The rows of images `imgs` (U-Net batch indices) of a per-call [nimg * HW, E] selection."""
+    return sel.view(nimg, -1, sel.shape[-1])[list(imgs)].reshape(-1, sel.shape[-1])
 
 
 def test_union_wanda_moe_sd14_64x64(parity_report):
     """Part 3 of the module docstring (config 4: multi_concept_remover.py:43-53 -> remove_wanda_neurons_fast.py:
-    69-83 on top of RemoveExperts routing): 2 prompts, 2 DDIM steps at 64x64, union of two concepts' Wanda masks
-    (baked per (t, l) in the experts' column order, the bench's default)."""
+    69-83 on top of RemoveExperts routing) at the bench's per-GPU shard: 8 prompts (U-Net batch 16), 2 DDIM steps at
+    64x64, union of two concepts' Wanda masks (baked per (t, l) in the experts' column order, the bench's default).
+    Same-input selection on all 16 images; the trunk vs the oracle on prompts 0 and 1 (their uncond / cond images
+    0, 1, 8, 9 of the batch, selection teacher-forced from those rows)."""
     from neuron_receivers import RemoveExperts, WandaRemoveNeuronsFast, MultiConceptRemoverWanda
     from oracle.unet_ref import UNetRef
     from conftest import heartbeat
@@ -277,7 +291,8 @@ def test_union_wanda_moe_sd14_64x64(parity_report):
     lists = removal_lists(mods, T, 63)
     rec = same_input_recorder(RemoveExperts)(0, None, T, L, expert_indices=lists, store_gates=False)
     rec.records = []
-    prompts = ["a church in the style of van gogh", "water lilies"]
+    prompts = ["a church in the style of van gogh", "water lilies"] + [f"synthetic prompt {i}" for i in range(2, 8)]
+    B = len(prompts)
     wanda.reset_time_layer()
     wanda.prepare(pipe)
     hooks = wanda.register_hooks(pipe)
@@ -289,13 +304,15 @@ def test_union_wanda_moe_sd14_64x64(parity_report):
     assert (wanda.timestep, wanda.layer) == (T, 0) and (rec.timestep, rec.layer) == (T, 0)
     assert all(m._out_keep is not None for m in mods), "fused routed path did not run under the Wanda hook"
     assert any(k[0] == "baked" and k[3] is False for k in wanda._dev if isinstance(k[0], str))
-    got = torch.stack(out).float().cpu()
-    with heartbeat("union 64x64 same-input"):
+    assert rec.records[0][2].shape[0] == 2 * B * 4096
+    got = torch.stack(out[:2]).float().cpu()
+    with heartbeat("union 64x64 b16 same-input"):
         tot = check_same_input(rec.records, mods, lists, "relu",
-                               report=lambda **tot: parity_report("same_input_selection_union_64x64", **tot))
-    # the trunk vs the oracle, with the device's selection teacher-forced on every row (selection itself was
-    # checked above on the device's own hook inputs)
-    sels = [sel_bits_to_bool(sb, mods[l].patterns.shape[0]) for t, l, _, sb, _ in rec.records]
+                               report=lambda **tot: parity_report("same_input_selection_union_64x64_b16", **tot))
+    # the trunk vs the oracle for prompts 0 and 1, with the device's selection teacher-forced on every row (selection
+    # itself was checked above on the device's own hook inputs)
+    imgs = (0, 1, B, B + 1)
+    sels = [image_rows(sel_bits_to_bool(sb, mods[l].patterns.shape[0]), 2 * B, imgs) for t, l, _, sb, _ in rec.records]
     rec.records = None
     del pipe
     torch.cuda.empty_cache()
@@ -309,9 +326,10 @@ def test_union_wanda_moe_sd14_64x64(parity_report):
         return hook
     stats = dict(rows=0, clear=0, clear_mismatch=0, forced=0)
     with heartbeat("union 64x64 oracle"):
-        exp = run_oracle(ref, cfg, prompts, T, ff_hook_factory=forced_factory(layers, "relu", sels, lists, stats),
+        exp = run_oracle(ref, cfg, prompts[:2], T, ff_hook_factory=forced_factory(layers, "relu", sels, lists, stats),
                          down_hook_factory=down_factory)
-    parity_report("union_wanda_moe_sd14_64x64", **tot, trunk_rel_l2=rel_l2(got, exp),
+    parity_report("union_wanda_moe_sd14_64x64_b16", **tot, trunk_rel_l2=rel_l2(got, exp),
                   trunk_clear_mismatch=stats["clear_mismatch"])
     assert stats["clear_mismatch"] == 0, stats
-    assert rel_l2(got, exp) <= 1e-2
+    # measured 3.96e-3 at 2 prompts (round 3): bound 8e-3
+    assert rel_l2(got, exp) <= 8e-3

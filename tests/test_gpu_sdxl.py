@@ -131,15 +131,21 @@ def test_unet_forward_sdxl_base_8x8():
     assert rel_l2(eps, r) <= 1e-2
 
 
-def test_pipeline_remove_experts_sdxl_base_128x128(parity_report):
+@pytest.mark.parametrize("act", ["gelu"])
+def test_pipeline_remove_experts_sdxl_base_128x128(act, parity_report):
     """BASELINE config 5 at its real shape: the SDXL-base U-Net at 1024^2 (4x128x128 latents: 4096-token d=64
-    self-attention at the 64x64 level, 10-deep transformers at 32x32), MoE-fied as the config-5 bench runs it (relufied,
-    top-k 0.2, expert 20 -> E = 128 / 256 on 70 FFNs), RemoveExperts skilled-expert mask (t < 20), one DDIM step with
-    CFG (U-Net batch 2) through the fused + keep routed FFN.
+    self-attention at the 64x64 level, 10-deep transformers at 32x32), MoE-fied as the config-5 bench runs it -- with
+    SDXL's own GELU FFN activation (the reference never relufies SDXL: utils.py:111-112 loads it as is, and the hook
+    applies module.gelu, remove_skilled_experts.py:27), top-k 0.2, expert 20 -> E = 128 / 256 on 70 FFNs --
+    RemoveExperts skilled-expert mask (t < 20), one DDIM step with CFG (U-Net batch 2) through the fused + keep routed
+    FFN (the routed-GEGLU epilogue evaluates the erf GELU).
     (1) Same-input selection (test_gpu_metric_parity's contract): every one of the 70 hooked calls re-run by the
         reference hook (fp16, CPU) on the device's own hook input: identical selection on every clear row and every
-        row with bit-equal scores, tie rows tie-consistent, >= 95 % of the rows compared.
-    (2) The trunk vs the fp32 oracle with the device's selection teacher-forced: latents rel L2 <= 1e-2."""
+        row with bit-equal scores, tie rows tie-consistent, >= 95 % of the rows compared, near-tie flips <= 1e-4 of
+        the rows.
+    (2) The trunk vs the fp32 oracle with the device's selection teacher-forced: latents rel L2 <= 1e-3 (measured
+        6.3e-5 relufied in round 3), and the oracle's own top-k on its own trunk agrees with the device's on every
+        row clear of a 16-ulp near-tie."""
     from neuron_receivers import GEGLU, RemoveExperts
     from conftest import heartbeat
     from test_gpu_metric_parity import same_input_recorder, check_same_input, teacher_forced_factory
@@ -148,7 +154,7 @@ def test_pipeline_remove_experts_sdxl_base_128x128(parity_report):
     with heartbeat("sdxl-128 weights"):
         unet, ref = build_rounded(cfg, seed=7)
     pipe = StableDiffusionPipeline(unet, DEV, num_inference_steps=1)
-    layers = moefy_tiny(pipe, topk=0.2, expert_size=20, relu=True)
+    layers = moefy_tiny(pipe, topk=0.2, expert_size=20, relu=act == "relu")
     mods = [m for n, m in pipe.unet.named_modules() if n.endswith("ff.net.0")]
     L = len(layers)
     assert L == 70 and {E for _, E, _ in layers} == {128, 256}
@@ -164,8 +170,8 @@ def test_pipeline_remove_experts_sdxl_base_128x128(parity_report):
     got = torch.stack(out).float().cpu()
     assert torch.isfinite(got).all()
     with heartbeat("sdxl-128 same-input"):
-        check_same_input(rec.records, mods, lists, "relu",
-                         report=lambda **tot: parity_report("same_input_selection_sdxl_base_128x128", **tot))
+        check_same_input(rec.records, mods, lists, act,
+                         report=lambda **tot: parity_report(f"same_input_selection_sdxl_base_128x128_{act}", **tot))
     sels = [sel_bits_to_bool(sb, mods[l].patterns.shape[0]) for t, l, _, sb, _ in rec.records]
     rec.records = None
     del pipe, unet, mods
@@ -176,7 +182,8 @@ def test_pipeline_remove_experts_sdxl_base_128x128(parity_report):
     stats = dict(rows=0, clear=0, clear_disagree=0)
     with heartbeat("sdxl-128 oracle"):
         exp = denoise(ref, lat, ctx[:B], ctx[B:], num_inference_steps=1, added_cond=ac,
-                      ff_hook_factory=teacher_forced_factory(layers, "relu", sels, lists, stats))
-    parity_report("pipeline_sdxl_base_128x128_remove_experts", rows=stats["rows"], clear=stats["clear"],
+                      ff_hook_factory=teacher_forced_factory(layers, act, sels, lists, stats))
+    parity_report(f"pipeline_sdxl_base_128x128_remove_experts_{act}", rows=stats["rows"], clear=stats["clear"],
                   oracle_trunk_clear_disagree=stats["clear_disagree"], rel_l2=rel_l2(got, exp))
-    assert rel_l2(got, exp) <= 1e-2
+    assert stats["clear_disagree"] == 0, stats
+    assert rel_l2(got, exp) <= 1e-3

@@ -113,6 +113,32 @@ def test_wanda_hook_on_reference_fixture(dtype, bake, parity_report):
     parity_report(f"wanda_hook_fixture[{dtype},{'baked' if bake else 'in_gemm'}]", layers=L, max_ulps=worst)
 
 
+def test_wanda_baked_weight_follows_in_place_update():
+    """An in-place update of ff.net.2's weight (load_state_dict / copy_ / a LoRA merge keeps the address) must
+    re-bake W * (1 - M): the cache is keyed by the Parameter's own version counter, not by `.data`'s."""
+    from neuron_receivers import WandaRemoveNeuronsFast
+    from sdmoe.unet import LoRACompatibleLinear
+    g = torch.Generator().manual_seed(5)
+    mask = (torch.rand(64, 256, generator=g) < 0.1).numpy()
+    rec = WandaRemoveNeuronsFast.from_packed(0, {0: {0: np.packbits(mask, axis=-1, bitorder="little")}}, 1, 1,
+                                             store_gates=False)
+    lin = LoRACompatibleLinear((torch.randn(64, 256, generator=g) * 0.05).half().to(DEV),
+                               torch.zeros(64, dtype=torch.float16, device=DEV))
+    x = torch.randn(128, 256, generator=g).half().to(DEV)
+    keep = torch.from_numpy(~mask).to(DEV)
+    y1 = rec.linear_hook_fn(lin, (x,), None)
+    assert torch.equal(y1, ops.linear(x, torch.where(keep, lin.weight, torch.zeros_like(lin.weight)), lin.bias))
+    ptr = lin.weight.data_ptr()
+    with torch.no_grad():
+        lin.weight.copy_(lin.weight * 2)  # in place: same address, new version
+    assert lin.weight.data_ptr() == ptr
+    rec.reset_time_layer()
+    y2 = rec.linear_hook_fn(lin, (x,), None)
+    assert any(isinstance(k[0], str) and k[0] == "baked" for k in rec._dev)
+    assert torch.equal(y2, ops.linear(x, torch.where(keep, lin.weight, torch.zeros_like(lin.weight)), lin.bias))
+    assert not torch.equal(y1, y2)
+
+
 @pytest.mark.parametrize("bake", [True, False], ids=["baked", "in_gemm"])
 def test_union_wanda_moe_pipeline_sd14(bake, parity_report):
     """Config 4's per-GPU path at SD-1.4 widths (32x32 latents, 2 prompts, 2 DDIM steps): a two-concept union Wanda

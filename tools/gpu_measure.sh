@@ -1,7 +1,9 @@
 #!/bin/bash
 # Round evidence on the GPU box, each step under its own limit, stopping at the first failure:
 #   bench        the metric run (bench line with roofline + cpu_baseline)
-#   union        --mask union (config 4)            sdxl       --model sdxl (config 5)
+#   union        --mask union (config 4)            sdxl       --model sdxl (config 5, GELU)
+#   none         --mask none (config 2, MOEFy)       b1 / b1none  --batch 1 with / without the mask (configs 3 / 2 at
+#                                                    the reference's one-prompt-per-call shape, base_receiver.py:73)
 #   prof         rocprofv3 --kernel-trace --stats of the metric run (prof_union / prof_sdxl likewise)
 #   pmc          FETCH_SIZE / WRITE_SIZE passes of a 2-step metric run -> pmc_conv_traffic.json
 # usage: gpurun -- bash tools/gpu_measure.sh TAG STEP...   (default steps: bench union prof)
@@ -27,11 +29,17 @@ for s in $STEPS; do
     bench) step bench 600 python bench.py --steps 10 --warmup 2 ;;
     union) step bench_union 600 python bench.py --mask union --steps 5 --warmup 1 $BA ;;
     sdxl) step bench_sdxl 600 python bench.py --model sdxl --steps 2 --warmup 1 $BA ;;
-    prof|prof_union|prof_sdxl)
+    none) step bench_none 600 python bench.py --mask none --steps 5 --warmup 1 $BA ;;
+    b1) step bench_b1 600 python bench.py --batch 1 --steps 10 --warmup 2 $BA ;;
+    b1none) step bench_b1none 600 python bench.py --batch 1 --mask none --steps 10 --warmup 2 $BA ;;
+    prof|prof_union|prof_sdxl|prof_none|prof_b1|prof_b1none)
       case $s in
         prof) args="--steps 5 --warmup 1" ;;
         prof_union) args="--mask union --steps 3 --warmup 1" ;;
         prof_sdxl) args="--model sdxl --steps 1 --warmup 1" ;;
+        prof_none) args="--mask none --steps 3 --warmup 1" ;;
+        prof_b1) args="--batch 1 --steps 5 --warmup 1" ;;
+        prof_b1none) args="--batch 1 --mask none --steps 5 --warmup 1" ;;
       esac
       cd /tmp && export TMPDIR=/tmp
       step $s 600 rocprofv3 --kernel-trace --stats -d $O/$s -o run --output-format csv -- python3 $R/bench.py $args $BA
