@@ -39,6 +39,27 @@ SDMOE_DEV float silu_f(float x) { return x / (1.0f + __expf(-x)); }
 // cancels in fp32 below x ~ -3); within 1 fp16 ulp of the correctly rounded value.
 SDMOE_DEV float gelu_erf_f(float x) { return 0.5f * x * erfcf(-x * 0.70710678118654752f); }
 
+// GELU of the reference's GEGLU (module.gelu = F.gelu on an fp16 tensor) over fp16 inputs, bit for bit: the
+// values for 2^-5 <= |x| < 8 come from a 16384-entry fp16 table -- the module's own activation evaluated on every
+// such input, registered per device by sdmoe_set_gelu_table -- at index (|x| bits - 0x2800) | sign << 13; below 2^-5
+// x * Phi(x) = 0.5 x + x^2 (1/sqrt(2 pi) - x^2 / (6 sqrt(2 pi))) in fp32 (next term 0.02 x^5 relative: < 1e-9);
+// x >= 8 -> x, x <= -8 -> -0 (fp32 erf saturates: the reference returns exactly these). One LDS (or L1) read and
+// ~10 VALU instead of erfcf's branchy polynomial + exp; also exact where the fp32 1 + erf form the reference
+// computes is not correctly rounded (0.9 % of fp16 inputs, mostly the negative tail).
+constexpr int GELU_TAB_N = 16384;
+SDMOE_DEV half_t gelu_tab_h(half_t x, const half_t* tab) {
+  const unsigned u = __builtin_bit_cast(unsigned short, x), a = u & 0x7fffu;
+  const float f = (float)x, x2 = f * f;
+  const half_t small = (half_t)__builtin_fmaf(x2, __builtin_fmaf(x2, -0.0664903745f, 0.3989422804f), 0.5f * f);
+  int idx = (int)a - 0x2800;
+  idx = idx < 0 ? 0 : (idx > 8191 ? 8191 : idx);
+  const half_t t = tab[idx | (int)((u >> 15) << 13)];
+  const half_t big = (u & 0x8000u) ? (half_t)(-0.0f) : x;
+  return a < 0x2800u ? small : (a >= 0x4800u ? big : t);
+}
+// the table registered for the calling thread's current device (gemm.hip), or null
+const half_t* sdmoe_gelu_tab_current();
+
 SDMOE_DEV float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -90,6 +90,8 @@ struct GemmParams {
   // W + i * w_bstride (0 = one weight set) and adds colf[i * colf_bstride + n] (fp32 per-image column add)
   long w_bstride;
   const float* colf; long colf_bstride;
+  // routed GEGLU with act == GELU: the registered fp16 GELU table (gelu_tab_h), staged into LDS for the epilogue
+  const half_t* gelu_tab;
 };
 
 SDMOE_DEV int swz(int row) { return (row >> 1) & 7; }
@@ -413,6 +415,23 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
     if constexpr (KEEP) bld16(rsK, sa + kdst, kvoff, (unsigned)ks * kstride);
   };
 
+  // routed GEGLU under GELU: the 32-KiB activation table goes to LDS by LDS-DMA (GELU_TAB_N / 512 pieces over the
+  // waves) -- during the last K-step into the top of the ring stage nothing reads then (stage nk % NSTAGE: consumed
+  // at step nk - NSTAGE, or never), when a stage holds it; otherwise after the main loop, behind the staging area
+  constexpr int TAB_BYTES = GELU_TAB_N * 2;
+  constexpr int G_STAGING = NW * 2 * (16 * (FM % 2 == 0 ? 2 : 1)) * (WN / 2) * 2 + NW * WN * 4;  // GEGLU epilogue
+  constexpr bool TAB_PREFETCH = GEGLU && STAGE >= TAB_BYTES && G_STAGING <= STAGE;
+  constexpr int TAB_LATE_OFF = ((G_STAGING + 1023) / 1024) * 1024;
+  constexpr bool TAB_OK = GEGLU && (TAB_PREFETCH || TAB_LATE_OFF + TAB_BYTES <= SMEM1);  // else apply_act's erfc
+  auto issue_gelu_tab = [&](char* dst) {
+    const __amdgpu_buffer_rsrc_t rsT = __builtin_amdgcn_make_buffer_rsrc((void*)p.gelu_tab, (short)0, TAB_BYTES, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < (TAB_BYTES / 1024 + NW - 1) / NW; ++j) {
+      const int piece = j * NW + wave;
+      if (piece < TAB_BYTES / 1024) bld16(rsT, dst + piece * 1024, (unsigned)(piece * 1024 + lane * 16), 0);
+    }
+  };
+
   // SWAP: C^T fragments (the MFMA's operands swapped): acc[i][j][r] = C[row wr*WM + 16 i + fr][col wc*WN + 16 j +
   // 4 fg + r], 4 consecutive output columns of one row per lane, so the epilogue works on half4 / float4 row pieces
   // (and the routed GEGLU pairs value / gate columns with one lane swap).
@@ -445,6 +464,7 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (it + NSTAGE - 1 < nk && !(p.diag & 1)) issue_stage(ks0 + it + NSTAGE - 1, (it + NSTAGE - 1) % NSTAGE);
+    else if (TAB_PREFETCH && it == nk - 1 && p.gelu_tab && p.act == ACT_GELU) issue_gelu_tab(smem + (nk % NSTAGE) * STAGE + STAGE - TAB_BYTES);
 
     const char* sa = smem + (it % NSTAGE) * STAGE;
     const char* sbm = sa + BM * BK * 2;
@@ -716,9 +736,23 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
     constexpr int GST = NW * 2 * RG * NH * 2;     // staging bytes of all waves
     static_assert(NH % 8 == 0, "whole 16-B product chunks per row");
     static_assert(GST + NW * WN * 4 <= SMEM1, "GEGLU staging and bias must fit in the kernel's LDS");
-    half_t* sp = reinterpret_cast<half_t*>(smem) + wave * 2 * RG * NH;  // products [RG][NH]
-    half_t* sg = sp + RG * NH;                                          // activated gates [RG][NH]
-    float* gbias = reinterpret_cast<float*>(smem + GST) + wave * WN;    // this wave's WN bias values (fp32)
+    // staging base: with the GELU table prefetched into ring stage nk % NSTAGE, the stage of the last K-step (free
+    // since the barrier above) holds the staging; otherwise offset 0 and a late-loaded table behind the staging
+    static_assert(GST + NW * WN * 4 == G_STAGING, "GEGLU staging size");
+    const bool gtab = TAB_OK && p.act == ACT_GELU && p.gelu_tab != nullptr;
+    char* const sbase = (TAB_PREFETCH && gtab) ? smem + ((nk - 1) % NSTAGE) * STAGE : smem;
+    const half_t* const tab = reinterpret_cast<const half_t*>(
+        TAB_PREFETCH ? smem + (nk % NSTAGE) * STAGE + STAGE - TAB_BYTES : smem + TAB_LATE_OFF);
+    if (!TAB_PREFETCH && gtab) {  // no stage holds the table: load it now (the ring is idle)
+      issue_gelu_tab(smem + TAB_LATE_OFF);
+    }
+    if (gtab) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // every wave's table pieces visible
+    }
+    half_t* sp = reinterpret_cast<half_t*>(sbase) + wave * 2 * RG * NH;  // products [RG][NH]
+    half_t* sg = sp + RG * NH;                                           // activated gates [RG][NH]
+    float* gbias = reinterpret_cast<float*>(sbase + GST) + wave * WN;    // this wave's WN bias values (fp32)
     for (int c = lane; c < WN; c += 64) gbias[c] = LN ? p.ln_bias[nw + c] : (float)p.bias[nw + c];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -734,8 +768,9 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
       bvv[j] = *reinterpret_cast<const float2v*>(gbias + 16 * j + nsel);
       bgg[j] = *reinterpret_cast<const float2v*>(gbias + 16 * j + 8 + nsel);
     }
-    auto stage_pass = [&](int h, auto relu_tag) {
-      constexpr bool RELU = decltype(relu_tag)::value;
+    auto stage_pass = [&](int h, auto act_tag) {
+      constexpr int ACTK = decltype(act_tag)::value;  // 0: ReLU, 1: GELU from the LDS table, 2: apply_act
+      constexpr bool RELU = ACTK == 0;
 #pragma unroll
       for (int ii = 0; ii < FPP; ++ii) {
         const int i = h * FPP + ii;
@@ -759,6 +794,7 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
           const h2 yg = {(half_t)(__uint_as_float(s02[1]) + bgg[j][0]), (half_t)(__uint_as_float(s13[1]) + bgg[j][1])};
           h2 ga;
           if constexpr (RELU) ga = __builtin_elementwise_max(yg, (h2){(half_t)0.f, (half_t)0.f});
+          else if constexpr (ACTK == 1) ga = (h2){gelu_tab_h(yg[0], tab), gelu_tab_h(yg[1], tab)};
           else ga = (h2){(half_t)apply_act((float)yg[0], p.act), (half_t)apply_act((float)yg[1], p.act)};
           const int off = (16 * ii + fr) * NH + 8 * j + nsel;
           *reinterpret_cast<h2*>(sp + off) = yv * ga;  // fp16 x fp16 is exact in fp32: rounds like the unfused path
@@ -768,8 +804,9 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
     };
 #pragma unroll
     for (int h = 0; h < FM / FPP; ++h) {
-      if (p.act == ACT_RELU) stage_pass(h, std::integral_constant<bool, true>());
-      else stage_pass(h, std::integral_constant<bool, false>());
+      if (p.act == ACT_RELU) stage_pass(h, std::integral_constant<int, 0>());
+      else if (gtab) stage_pass(h, std::integral_constant<int, 1>());
+      else stage_pass(h, std::integral_constant<int, 2>());
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1121,12 +1158,32 @@ __global__ __launch_bounds__(256) void gn_fold_kernel(const half_t* __restrict__
   if (lane == 0) colbias[(long)img * N + n] = acc + (bias ? (float)bias[n] : 0.f);
 }
 
+// fp16 GELU tables registered per device (sdmoe_set_gelu_table)
+constexpr int MAX_DEV = 64;
+const void* g_gelu_tab[MAX_DEV] = {};
+
 int grid_for(long n) {
   long g = (n + 255) / 256;
   return (int)(g > 4096 ? 4096 : (g < 1 ? 1 : g));
 }
 
 }  // namespace
+
+const half_t* sdmoe_gelu_tab_current() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEV) return nullptr;
+  return (const half_t*)g_gelu_tab[dev];
+}
+
+extern "C" int sdmoe_set_gelu_table(const void* table) {
+  int dev = 0;
+  const hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return (int)e;
+  if (dev < 0 || dev >= MAX_DEV) return SDMOE_EARG;
+  if (table && (reinterpret_cast<uintptr_t>(table) & 15)) return SDMOE_ESHAPE;
+  g_gelu_tab[dev] = table;
+  return SDMOE_OK;
+}
 
 extern "C" int sdmoe_linear(const void* A, long lda, const void* W, long ldw, const void* bias,
                             const void* coladd, long coladd_bstride, int rows_per_batch,
@@ -1223,6 +1280,7 @@ extern "C" int sdmoe_linear_geglu(const void* A, long lda, const void* W, long l
   p.bias = (const half_t*)bias; p.C = (half_t*)P; p.ldc = ldp;
   p.M = M; p.N = 2 * F; p.K = K; p.act = act; p.rows_per_batch = 1;
   p.score = (half_t*)score; p.ld_score = ld_score; p.esize = esize;
+  if (act == ACT_GELU) p.gelu_tab = sdmoe_gelu_tab_current();
   const long ab = ((long)(M - 1) * lda + K) * 2, wb = ((long)(2 * F - 1) * ldw + K) * 2;
   if (ab >= (long)OOB || wb >= (long)OOB) return SDMOE_ESHAPE;
   p.a_bytes = (int)ab; p.w_bytes = (int)wb;
@@ -1270,6 +1328,7 @@ extern "C" int sdmoe_linear_geglu_ln(const void* A, long lda, const void* W, lon
   p.M = M; p.N = 2 * F; p.K = K; p.act = act; p.rows_per_batch = 1;
   p.score = (half_t*)score; p.ld_score = ld_score; p.esize = esize;
   p.ln_wsum = wsum; p.ln_bias = bias_f; p.ln_eps = eps;
+  if (act == ACT_GELU) p.gelu_tab = sdmoe_gelu_tab_current();
   const long ab = ((long)(M - 1) * lda + K) * 2, wb = ((long)(2 * F - 1) * ldw + K) * 2;
   if (ab >= (long)OOB || wb >= (long)OOB) return SDMOE_ESHAPE;
   p.a_bytes = (int)ab; p.w_bytes = (int)wb;

@@ -28,6 +28,7 @@ struct RouteParams {
   half_t* gate_out; long ldg;
   uint32_t* sel_out;        // [M][ceil(E/32)] or null (top-k result, before the removal mask)
   half_t* score_out;        // [M][E] or null
+  const half_t* gelu_tab;   // act == GELU: the registered fp16 GELU table (gelu_tab_h), or null (erfc form)
 };
 
 SDMOE_DEV uint32_t order_key(half_t s) {
@@ -54,7 +55,7 @@ __global__ __launch_bounds__(256) void geglu_route_kernel(RouteParams p) {
     half8 v = *reinterpret_cast<const half8*>(yrow + F + 8 * c);
     half8 o;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = (half_t)apply_act((float)v[j], p.act);
+    for (int j = 0; j < 8; ++j) o[j] = p.gelu_tab ? gelu_tab_h(v[j], p.gelu_tab) : (half_t)apply_act((float)v[j], p.act);
     *reinterpret_cast<half8*>(gact + 8 * c) = o;
   }
   __syncthreads();
@@ -352,7 +353,8 @@ extern "C" int sdmoe_geglu_route(const void* Y, long ldy, int M, int F, int E, i
   if (E > 0 && (!labels || !e_off || !e_nid || k < 0 || k > E)) return SDMOE_EARG;
   if (!(act == ACT_GELU || act == ACT_RELU || act == ACT_NONE || act == ACT_SILU)) return SDMOE_EUNSUP;
   RouteParams p{(const half_t*)Y, ldy, M, F, E, k, act, labels, e_off, e_nid, removed_bits,
-                (half_t*)out, ldo, (half_t*)gate_out, ldg, sel_out, (half_t*)score_out};
+                (half_t*)out, ldo, (half_t*)gate_out, ldg, sel_out, (half_t*)score_out,
+                act == ACT_GELU ? sdmoe_gelu_tab_current() : nullptr};
   const size_t smem = (size_t)4 * F * sizeof(half_t) + 4 * 8 * sizeof(uint32_t);
   if (smem > 160 * 1024) return SDMOE_ESHAPE;
   hipStream_t s = (hipStream_t)stream;

@@ -57,6 +57,7 @@ SIGNATURES = {
     "sdmoe_cfg_ddim_step": [_P, _L, _P, _I, _I, _I, _F, _F, _F, _P, _L, _P],
     "sdmoe_add": [_P, _P, _P, _L, _P],
     "sdmoe_tune": [_I, _I],
+    "sdmoe_set_gelu_table": [_P],
     "sdmoe_version": [],
 }
 

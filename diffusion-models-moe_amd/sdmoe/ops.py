@@ -472,11 +472,42 @@ def interleave_ln_fold(fold: LNFold, perm: torch.Tensor | None) -> LNFold:
     return fold.rows(rows)
 
 
+_GELU_TABLES = {}
+
+
+def gelu_table_values() -> torch.Tensor:
+    """The 16384 fp16 inputs x with 2^-5 <= |x| < 8 in sdmoe_set_gelu_table's index order (int16 bit patterns:
+    index i -> |x| bits 0x2800 + (i & 8191), sign i >> 13), as an fp16 CPU tensor."""
+    i = torch.arange(16384, dtype=torch.int32)
+    bits = (0x2800 + (i & 8191)) | ((i >> 13) << 15)
+    return bits.to(torch.int16).view(torch.float16)
+
+
+def ensure_gelu_table(device) -> torch.Tensor:
+    """Register (once per device) the GELU table the GEGLU kernels apply for act == GELU: the reference module's
+    activation itself -- diffusers GEGLU.gelu is F.gelu, which the hook applies to the fp16 gate (moefy.py:13,
+    remove_skilled_experts.py:27) -- evaluated on every fp16 input of the table's range, so the device gates equal
+    the reference's fp16 gates bit for bit (sdmoe_set_gelu_table, include/sdmoe.h). Must run outside graph capture
+    (one host->device copy); the first GELU call on a device does it."""
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    t = _GELU_TABLES.get(idx)
+    if t is None:
+        vals = torch.nn.functional.gelu(gelu_table_values())  # fp16 CPU, as the reference's fp16 gate
+        t = vals.to(torch.device("cuda", idx)).contiguous()
+        with torch.cuda.device(idx):
+            _lib.check(_lib.load().sdmoe_set_gelu_table(t.data_ptr()), "sdmoe_set_gelu_table")
+        _GELU_TABLES[idx] = t
+    return t
+
+
 def linear_geglu(x, w_il, b_il, act=ACT_GELU, *, score=None, esize=0, out=None, ln: LNFold | None = None):
     """P = value * act(gate) from the interleaved projection (interleave_geglu), plus per-expert gate sums
     into score [M, E] (experts = contiguous esize-neuron slices) when given. ln (interleave_ln_fold): x is the
     un-normalised input and the LayerNorm is folded into the GEMM (w_il / b_il are then ignored)."""
     lib = _lib.load()
+    if act == ACT_GELU:
+        ensure_gelu_table(x.device)
     if ln is not None:
         xp, lda = _rows(x, "x")
         M, K = x.shape
@@ -572,6 +603,8 @@ def geglu_route(y, routing: Routing | None, act=ACT_GELU, removed=None, out=None
     """Routed GEGLU over y = proj(x) [M, 2F]; routing None -> dense value*act(gate). k overrides routing.k
     (k = E: every expert kept, i.e. the dense product plus the per-token expert scores)."""
     lib = _lib.load()
+    if act == ACT_GELU:
+        ensure_gelu_table(y.device)
     yp, ldy = _rows(y, "y")
     M = y.shape[0]
     F = y.shape[1] // 2

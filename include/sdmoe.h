@@ -349,6 +349,19 @@ int sdmoe_cfg_multistep_step(const void* eps, long lde, float* lat, int B, int H
    one / four tokens per wave. */
 int sdmoe_tune(int knob, int value);
 
+/*
+ * Registers, for the calling thread's current HIP device, the fp16 GELU table the GEGLU kernels apply for
+ * act == SDMOE_ACT_GELU (sdmoe_linear_geglu / _ln, sdmoe_geglu_route): table[i] = gelu(x) for the 16384 fp16 inputs
+ * x with 2^-5 <= |x| < 8, i = ((bits(x) & 0x7fff) - 0x2800) | (sign(x) << 13), device memory, 16-B aligned, kept
+ * alive by the caller while registered (NULL unregisters: the kernels then evaluate 0.5 x erfc(-x / sqrt 2) in
+ * fp32, within 1 fp16 ulp). The host layer fills it with the reference module's own activation (GEGLU.gelu =
+ * F.gelu on fp16 tensors, diffusers activations.py; the hook's module.gelu(gate), remove_skilled_experts.py:27,
+ * moefy.py:13) evaluated on every such input, so the fused routed GEGLU reproduces the reference's fp16 gate
+ * values bit for bit on all of them; |x| < 2^-5, |x| >= 8 are computed (see csrc/common.h gelu_tab_h).
+ * No GPU call; not stream-ordered: register before launching work that reads it.
+ */
+int sdmoe_set_gelu_table(const void* table);
+
 /* out = a + b (fp16, n % 8 == 0). */
 int sdmoe_add(const void* a, const void* b, void* out, long n, void* stream);
 

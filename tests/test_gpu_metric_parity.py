@@ -8,7 +8,9 @@
    once) is re-run on exactly those inputs. So the trunk's fp16-vs-fp32 drift plays no part: the selection must
    be identical on every row except
      * exact ties at the k-th score, where torch.topk's order is implementation-defined: the device's choice must
-       be a valid top-k of the reference's scores (tie-consistent);
+       be a valid top-k of the reference's scores (tie-consistent) -- or, when the device's scores differ from the
+       reference's (a 0-ulp near-tie: GELU's last-ulp rounding differs between the device and the CPU), it is
+       counted as a near-tie flip;
      * rows whose k-th/(k+1)-th gap is within 2 fp16 ulps AND whose device scores differ from the reference's:
        our projection GEMM sums in another fp32 order, so a y element can sit one ulp away and move a score by an
        ulp. Those flips are counted and reported.
@@ -74,7 +76,7 @@ def check_same_input(records, mods, lists, act, min_compared=0.95, report=None, 
     whose device scores differ from the reference's) are bounded: at most max_flip_frac of all rows (measured: 6 of
     862,208 at the SD-1.4 batch-16 workload, 2 of 204,800 for SDXL 1024^2, 1 of 215,552 for the union)."""
     tot = dict(rows=0, compared=0, clear=0, exact_tie=0, tie_consistent=0, near_tie=0, near_tie_equal_scores=0,
-               near_tie_flips=0, score_bit_equal_rows=0, calls=0)
+               near_tie_flips=0, tie_flips=0, score_bit_equal_rows=0, calls=0)
     weights = {}
     for t, l, x, sel_bits, dscore in records:
         m = mods[l]
@@ -114,7 +116,10 @@ def check_same_input(records, mods, lists, act, min_compared=0.95, report=None, 
         # ties toward the lowest expert id, so the selection must be identical (near-tie and tie rows included)
         score_eq = (so == sd).all(1)
         assert not (score_eq & mism).any(), f"(t={t}, l={l}): equal scores, different selection"
-        assert consistent[tie].all(), f"(t={t}, l={l}): a tie row's selection is not a valid top-k"
+        # an exact tie in the reference's scores that the device's (different: GELU's last-ulp rounding, the GEMM's
+        # fp32 order) scores resolve another way is a near-tie at a 0-ulp gap: counted with the near-tie flips
+        tie_flip = tie & ~consistent
+        assert not (tie_flip & score_eq).any()
         tot["rows"] += tie.size
         tot["calls"] += 1
         tot["clear"] += int(clear.sum())
@@ -122,7 +127,8 @@ def check_same_input(records, mods, lists, act, min_compared=0.95, report=None, 
         tot["tie_consistent"] += int((tie & consistent).sum())
         tot["near_tie"] += int(near.sum())
         tot["near_tie_equal_scores"] += int((near & score_eq).sum())
-        tot["near_tie_flips"] += int((near & mism).sum())
+        tot["near_tie_flips"] += int((near & mism).sum()) + int(tie_flip.sum())
+        tot["tie_flips"] += int(tie_flip.sum())
         tot["score_bit_equal_rows"] += int(score_eq.sum())
         tot["compared"] += int((clear | (near & score_eq) | (tie & consistent)).sum())
     if report is not None:

@@ -212,7 +212,8 @@ def _fused(x, w, b, routing, act, removed=None):
 
 @pytest.mark.parametrize("M,C,E,k,act,nrem", [(4096, 320, 64, 12, ops.ACT_GELU, 0), (1000, 320, 64, 12, ops.ACT_RELU, 5),
                                               (2048, 640, 128, 25, ops.ACT_GELU, 9), (512, 1280, 256, 51, ops.ACT_GELU, 20),
-                                              (333, 640, 128, 128, ops.ACT_RELU, 0)])
+                                              (333, 640, 128, 128, ops.ACT_RELU, 0), (256, 320, 64, 12, ops.ACT_GELU, 3),
+                                              (8192, 640, 128, 25, ops.ACT_GELU, 9)])
 def test_fused_geglu_bit_exact_vs_unfused(M, C, E, k, act, nrem):
     """Same rounding points and the same neuron-order fp32 score sums as proj GEMM + sdmoe_geglu_route:
     output, scores and top-k bits are bit-identical (no split-K at K = C, so the GEMM sums agree too)."""
@@ -301,6 +302,40 @@ def test_topk_one_token_per_wave_matches_four(M, E, k, nrem):
     for a_, b_ in zip(res[0], res[4]):
         assert torch.equal(a_, b_)
     assert torch.equal(res[0][1], res[0][2])
+
+
+@pytest.mark.parametrize("M", [64, 4096, 8192])  # 64x160 (table loaded after the K loop), 128x160, 256x320 tiles
+def test_gelu_every_fp16_input_matches_reference_activation(M):
+    """The GEGLU kernels' GELU on EVERY finite fp16 gate value vs the reference's activation itself (F.gelu on an fp16
+    tensor: diffusers GEGLU.gelu, the hook's module.gelu(gate), moefy.py:13): sdmoe_geglu_route (gate_out) and the
+    fused routed-GEGLU epilogue (value 1.0, so P = gelu(gate)) are bit-identical to it on all but <= 2 inputs (the fp32
+    series below 2^-5, tests/test_host_logic.py::test_gelu_table_reproduces_reference_activation), and to each other.
+    The fused GEMM is driven so that its gate outputs are exact chosen fp16 values: x rows are unit vectors e_(m % 64)
+    and W's gate rows hold the values (one fp16 product per fp32 sum)."""
+    allx = torch.arange(65536, dtype=torch.int32).to(torch.int16).view(torch.float16)
+    allx = allx[torch.isfinite(allx)]
+    F = 1280
+    vals = torch.zeros(64 * F, dtype=torch.float16)
+    vals[:allx.numel()] = allx
+    gate = vals.view(64, F)                                   # gate[j, n]: the value row j of x selects
+    ref = torch.nn.functional.gelu(gate)                      # the reference's fp16 GELU (CPU)
+    # unfused: y = [value 1.0 | gate]
+    y = torch.cat([torch.ones(64, F, dtype=torch.float16), gate], 1).to(DEV)
+    g_out = torch.empty((64, F), dtype=torch.float16, device=DEV)
+    ops.geglu_route(y, None, ops.ACT_GELU, gate_out=g_out)
+    got_u = g_out.cpu()
+    # fused: x = e_(m % 64) (K = 64), W = [ones | gate^T] rows, bias 0
+    x = torch.zeros(M, 64, dtype=torch.float16)
+    x[torch.arange(M), torch.arange(M) % 64] = 1.0
+    w = torch.cat([torch.ones(F, 64, dtype=torch.float16), gate.t().contiguous()], 0).to(DEV)
+    w_il, b_il = ops.interleave_geglu(w, torch.zeros(2 * F, dtype=torch.float16, device=DEV), None)
+    P = ops.linear_geglu(x.to(DEV), w_il, b_il, ops.ACT_GELU).cpu()
+    exp_rows = torch.arange(M) % 64
+    assert torch.equal(P, got_u[exp_rows])                    # fused == unfused, bit for bit
+    same = (got_u.view(torch.int16) == ref.view(torch.int16)) | ((got_u == 0) & (ref == 0))
+    bad = gate[~same]
+    assert (~same).sum().item() <= 2, bad
+    assert bool((bad.float().abs() < 2.0 ** -5).all())
 
 
 def test_fused_geglu_dense_matches_unfused():

@@ -500,3 +500,89 @@ def test_bench_roofline_timer_samples_whole_evaluations():
     assert seen[0] is False
     assert [i for i, on in enumerate(seen[1:]) if on] == [0, 10, 20]
     assert timer.evals == 25 and timer.sampled_evals == 3 and timer.on_eval is False
+
+
+def _gelu_tab_h_np(x16, tab):
+    """numpy restatement of csrc/common.h gelu_tab_h over fp16 inputs (fmaf emulated in float64, exact here: the
+    products of two float32 values are exact in float64 and the sums round once to float32 below)."""
+    u = x16.view(np.uint16).astype(np.int64)
+    a = u & 0x7FFF
+    np.seterr(over="ignore")  # the series is evaluated (and discarded) for every input, huge ones included
+    f = x16.astype(np.float32).astype(np.float64)
+    x2 = np.float32(f * f).astype(np.float64)
+    inner = np.float32(x2 * np.float64(np.float32(-0.0664903745)) + np.float64(np.float32(0.3989422804)))
+    small = np.float32(x2 * inner.astype(np.float64) + np.float64(np.float32(0.5 * f))).astype(np.float16)
+    idx = np.clip(a - 0x2800, 0, 8191) | ((u >> 15) << 13)
+    t = tab[idx]
+    big = np.where(u & 0x8000, np.float16(-0.0), x16)
+    return np.where(a < 0x2800, small, np.where(a >= 0x4800, big, t))
+
+
+def test_gelu_table_reproduces_reference_activation():
+    """The GEGLU kernels' GELU (csrc/common.h gelu_tab_h + the table ops.ensure_gelu_table registers) against the
+    reference's own fp16 activation (F.gelu on an fp16 tensor: diffusers GEGLU.gelu, the hook's module.gelu(gate)) on
+    EVERY finite fp16 input: the table covers 2^-5 <= |x| < 8 by construction; the fp32 series below 2^-5 and the
+    saturated ends must reproduce F.gelu too (bit for bit up to a documented handful of inputs)."""
+    import torch.nn.functional as F
+    from sdmoe import ops
+    xs_tab = ops.gelu_table_values()
+    assert xs_tab.dtype == torch.float16 and xs_tab.numel() == 16384
+    a = xs_tab.view(torch.int16).numpy().astype(np.int64) & 0x7FFF
+    assert a.min() == 0x2800 and a.max() == 0x47FF  # 2^-5 <= |x| < 8
+    tab = F.gelu(xs_tab).numpy()
+    allx = np.arange(65536, dtype=np.uint32).astype(np.uint16).view(np.float16)
+    allx = allx[np.isfinite(allx)]
+    ref = F.gelu(torch.from_numpy(allx.copy())).numpy()
+    got = _gelu_tab_h_np(allx, tab)
+    same = (got.view(np.uint16) == ref.view(np.uint16)) | ((got == 0) & (ref == 0))
+    bad = allx[~same]
+    # everything bit-identical except inputs outside the table whose fp32 series rounds the other way (measured: 1)
+    assert (~same).sum() <= 2, bad
+    assert np.all(np.abs(bad.astype(np.float32)) < 2.0 ** -5)
+    ulps = np.abs(got[~same].astype(np.float32) - ref[~same].astype(np.float32)) / np.spacing(np.abs(ref[~same]))
+    assert np.all(ulps <= 1.0)
+
+
+def test_step_graph_counter_emulation():
+    """StepGraphs (sdmoe/pipeline.py): the hook owners a replay must emulate are sdmoe receivers without host-side
+    gate capture (anything else disables graphs); each replayed step checks the owners' (timestep, layer) counter
+    against its capture-time value and sets the post-step value, as the eager hooks would."""
+    from sdmoe.pipeline import StepGraphs, hook_owners
+    from neuron_receivers import RemoveExperts, MOEFy
+
+    class Box(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a, self.b = torch.nn.Identity(), torch.nn.Identity()
+    unet = Box()
+    rec = RemoveExperts(0, None, 2, 2, expert_indices={t: {l: [] for l in range(2)} for t in range(2)},
+                        store_gates=False)
+    assert hook_owners(unet) == []
+    h1 = unet.a.register_forward_hook(rec.hook_fn)
+    h2 = unet.b.register_forward_hook(rec.hook_fn)
+    assert hook_owners(unet) == [rec]
+    gates = MOEFy(0, store_gates=True)
+    h3 = unet.a.register_forward_hook(gates.hook_fn)
+    assert hook_owners(unet) is None  # gate capture -> no graphs
+    h3.remove()
+    h4 = unet.b.register_forward_hook(lambda m, i, o: o)
+    assert hook_owners(unet) is None  # a foreign hook -> no graphs
+    h4.remove()
+
+    class FakeGraph:
+        def __init__(self, log, i):
+            self.log, self.i = log, i
+
+        def replay(self):
+            self.log.append((self.i, rec.timestep, rec.layer))
+    log = []
+    st = StepGraphs([rec])
+    st.graphs = [FakeGraph(log, 0), FakeGraph(log, 1)]
+    st.counters = [([(0, 0)], [(1, 0)]), ([(1, 0)], [(2, 0)])]
+    rec.reset_time_layer()
+    st.replay()
+    assert log == [(0, 0, 0), (1, 1, 0)] and (rec.timestep, rec.layer) == (2, 0)
+    with pytest.raises(RuntimeError, match="counter"):
+        st.replay()  # not reset: the first step's captured pre-state (0, 0) does not match
+    h1.remove()
+    h2.remove()
