@@ -50,7 +50,9 @@ constexpr int GELU_TAB_N = 16384;
 SDMOE_DEV half_t gelu_tab_h(half_t x, const half_t* tab) {
   const unsigned u = __builtin_bit_cast(unsigned short, x), a = u & 0x7fffu;
   const float f = (float)x, x2 = f * f;
-  const half_t small = (half_t)__builtin_fmaf(x2, __builtin_fmaf(x2, -0.0664903745f, 0.3989422804f), 0.5f * f);
+  float sf = __builtin_fmaf(x2, __builtin_fmaf(x2, -0.0664903745f, 0.3989422804f), 0.5f * f);
+  asm volatile("" : "+v"(sf));  // round to fp32 first (as the reference): no fused fma -> f16 (v_fma_mix) rounding
+  const half_t small = (half_t)sf;
   int idx = (int)a - 0x2800;
   idx = idx < 0 ? 0 : (idx > 8191 ? 8191 : idx);
   const half_t t = tab[idx | (int)((u >> 15) << 13)];

@@ -40,6 +40,7 @@ int g_res16 = 1;  // knob 8: 1 = residual epilogues on the fp16 staging path (re
 int g_ksplit = 0;  // knob 9: forced split-K factor (0 = auto; 1 = never split), for tile sweeps
 int g_mfast = 1;   // knob 14: split-K conv grids ordered M-tile fastest (1) or split fastest (0)
 int g_diag = 0;  // knob 6, diagnostics only (results garbage): bit 0 = no K-loop operand loads, bit 1 = no MFMAs,
+                 // bit 4 = no A-operand pieces, bit 5 = no B-operand pieces,
                  // bit 2 = no epilogue (nothing stored), bit 3 = epilogue without its global stores
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -377,7 +378,8 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
   auto issue_stage = [&](int ks, int buf) {
     char* sa = smem + buf * STAGE;
     const unsigned kb = (unsigned)(ks * BK * 2);
-    if (!CONV) {
+    if (p.diag & 16) {  // diagnostics: no A pieces (B only)
+    } else if (!CONV) {
 #pragma unroll
       for (int j = 0; j < A_PW; ++j) bld16(rsA, sa + a_dst(j), avoff[j], kb);
     } else if (MODE == MODE_CONV && st_c >= csl) {  // folded shortcut K-step (wave-uniform)
@@ -410,8 +412,10 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
         }
       }
     }
+    if (!(p.diag & 32)) {  // diagnostics: bit 5 = no B pieces (A only)
 #pragma unroll
-    for (int j = 0; j < B_PW; ++j) bld16(rsW, sa + b_dst(j), bvoff[j], kb);
+      for (int j = 0; j < B_PW; ++j) bld16(rsW, sa + b_dst(j), bvoff[j], kb);
+    }
     if constexpr (KEEP) bld16(rsK, sa + kdst, kvoff, (unsigned)ks * kstride);
   };
 
@@ -1426,7 +1430,7 @@ extern "C" int sdmoe_tune(int knob, int value) {
   if (knob == 14 && (value == 0 || value == 1)) { g_mfast = value; return SDMOE_OK; }
   if (knob == 2 && (value == 0 || value == 32 || value == 64)) { g_bk = value; return SDMOE_OK; }
   if (knob == 3 && (value == 0 || value == 1)) { g_prio = value; return SDMOE_OK; }
-  if (knob == 6 && value >= 0 && value <= 15) { g_diag = value; return SDMOE_OK; }
+  if (knob == 6 && value >= 0 && value <= 63) { g_diag = value; return SDMOE_OK; }
   if (knob == 8 && (value == 0 || value == 1)) { g_res16 = value; return SDMOE_OK; }
   if (knob == 15 && (value == 0 || value == 1 || value == 4)) { g_topk_tpw = value; return SDMOE_OK; }
   return SDMOE_EARG;

@@ -334,7 +334,7 @@ def test_gelu_every_fp16_input_matches_reference_activation(M):
     assert torch.equal(P, got_u[exp_rows])                    # fused == unfused, bit for bit
     same = (got_u.view(torch.int16) == ref.view(torch.int16)) | ((got_u == 0) & (ref == 0))
     bad = gate[~same]
-    assert (~same).sum().item() <= 2, bad
+    assert (~same).sum().item() <= 1, bad  # the CPU restatement's count (+-2^-24 ties, test_host_logic)
     assert bool((bad.float().abs() < 2.0 ** -5).all())
 
 

@@ -536,8 +536,9 @@ def test_gelu_table_reproduces_reference_activation():
     got = _gelu_tab_h_np(allx, tab)
     same = (got.view(np.uint16) == ref.view(np.uint16)) | ((got == 0) & (ref == 0))
     bad = allx[~same]
-    # everything bit-identical except inputs outside the table whose fp32 series rounds the other way (measured: 1)
-    assert (~same).sum() <= 2, bad
+    # everything bit-identical except inputs outside the table whose fp32 series rounds the other way (measured: 1,
+    # x = 2^-24, whose gelu is an exact fp16 tie that torch's vectorised erf form rounds up)
+    assert (~same).sum() <= 1, bad
     assert np.all(np.abs(bad.astype(np.float32)) < 2.0 ** -5)
     ulps = np.abs(got[~same].astype(np.float32) - ref[~same].astype(np.float32)) / np.spacing(np.abs(ref[~same]))
     assert np.all(ulps <= 1.0)
