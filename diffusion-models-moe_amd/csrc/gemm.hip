@@ -153,7 +153,12 @@ SDMOE_DEV void epilogue8(const GemmParams& p, int m, int n, float (&v)[8]) {
 // WMASK: W operand masked per (row, k) by Wanda bits; KEEPW: both (the routed FFN down projection under a Wanda mask)
 // GEMM_LN / GEGLU_LN: GEMM / GEGLU with the LayerNorm of the A rows folded in (row statistics from the A tiles)
 enum { MODE_GEMM = 0, MODE_CONV = 1, MODE_CONV_UP = 2, MODE_GEGLU = 3, MODE_KEEP = 4, MODE_WMASK = 5, MODE_KEEPW = 6,
-       MODE_GEMM_LN = 7, MODE_GEGLU_LN = 8 };
+       MODE_GEMM_LN = 7, MODE_GEGLU_LN = 8, MODE_CONVH64 = 9, MODE_CONVH32 = 10, MODE_CONVH16 = 11 };
+// halo-tiled stride-1 3x3 conv (MODE_CONVH<W>, image width W): a tile is BM / W whole output rows of one image; per
+// 32-channel slice the (BM / W + 2) x (W + 2) input halo is staged in LDS ONCE and read by all 9 taps at shifted
+// rows, instead of 9 shifted A tiles (A pieces per K-step 27/9 instead of BM / 16)
+constexpr bool mode_halo(int mode) { return mode >= MODE_CONVH64 && mode <= MODE_CONVH16; }
+constexpr int halo_w(int mode) { return mode == MODE_CONVH64 ? 64 : (mode == MODE_CONVH32 ? 32 : 16); }
 constexpr bool mode_akeep(int mode) { return mode == MODE_KEEP || mode == MODE_KEEPW; }
 constexpr bool mode_wmask(int mode) { return mode == MODE_WMASK || mode == MODE_KEEPW; }
 
@@ -238,16 +243,22 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
   constexpr int STAGE = KEEP_OFF + keep_stage_bytes<BM, BN, MODE>();
   // epilogue staging: fp16 final values (row stride RS16 halves: 16-B aligned rows, conflict-free b64 stores of the
   // swapped fragments) in NPASS16 passes; the fp32 path (activation, residual) in NPASS passes; GEGLU: its own passes
+  // halo conv (MODE_CONVH*): two halo buffers of H_INS pieces (input rows BM / HW_ + 2 at a pitch of HW_ + 8 pixels: a
+  // multiple of 8 rows, so a fragment's swizzle depends only on its lane and tap column) + an NSTAGE ring of B tiles
+  constexpr bool HALO = mode_halo(MODE);
+  constexpr int HW_ = halo_w(MODE), HP = HW_ + 8, HR = BM / HW_;
+  constexpr int H_INS = HALO ? ((HR + 2) * HP + RPP - 1) / RPP : 0;
+  constexpr int HBYTES = H_INS * 1024, BSTAGE = BN * RB;
+  constexpr int RING = HALO ? 2 * HBYTES + NSTAGE * BSTAGE : NSTAGE * STAGE;  // main-loop LDS
   constexpr int RS16 = WN + 8;
-  constexpr int NPASS16 = (NW * WM * RS16 * 2 <= NSTAGE * STAGE) ? 1 : (NW * (WM / 2) * RS16 * 2 <= NSTAGE * STAGE) ? 2
-                          : ((NW * (WM / 4) * RS16 * 2 <= NSTAGE * STAGE) ? 4 : 8);
+  constexpr int NPASS16 = (NW * WM * RS16 * 2 <= RING) ? 1 : (NW * (WM / 2) * RS16 * 2 <= RING) ? 2
+                          : ((NW * (WM / 4) * RS16 * 2 <= RING) ? 4 : 8);
   constexpr int WN_PAD = WN + 4;
-  constexpr int NPASS = (NW * (WM / 2) * WN_PAD * 4 <= NSTAGE * STAGE) ? 2 : ((NW * (WM / 4) * WN_PAD * 4 <= NSTAGE * STAGE) ? 4 : 8);
+  constexpr int NPASS = (NW * (WM / 2) * WN_PAD * 4 <= RING) ? 2 : ((NW * (WM / 4) * WN_PAD * 4 <= RING) ? 4 : 8);
   static_assert(FM % NPASS == 0 && FM % NPASS16 == 0, "epilogue passes must split the wave's fragment rows");
   constexpr int EPI = NW * (WM / NPASS) * WN_PAD * 4;
   constexpr int EPI16 = NW * (WM / NPASS16) * RS16 * 2;
-  constexpr int SMEM0 = (NSTAGE * STAGE > EPI) ? (NSTAGE * STAGE > EPI16 ? NSTAGE * STAGE : EPI16)
-                                              : (EPI > EPI16 ? EPI : EPI16);
+  constexpr int SMEM0 = (RING > EPI) ? (RING > EPI16 ? RING : EPI16) : (EPI > EPI16 ? EPI : EPI16);
   constexpr int LUT_OFF = SMEM0;                 // MODE_KEEP: 16-entry nibble -> lane-mask table behind everything
   constexpr int SMEM1 = SMEM0 + (KEEP ? KEEP_LUT_BYTES : 0);
   // LN: per tile row (rstd, -mean*rstd), then the tile's BN columns of wsum and ln_bias (fp32), behind everything
@@ -446,12 +457,131 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = (float4v){0.f, 0.f, 0.f, 0.f};
 
+  const int fr = lane & 15, fg = lane >> 4;
+  if constexpr (HALO) {
+    // ---- halo-tiled 3x3 conv main loop. K-step = (32-channel slice c, tap t); the 9 taps of a slice are unrolled
+    // (kh, kw, ring stage t % 3 compile-time). Per iteration: counted wait for B(ks) (and the slice's halo, always
+    // older), one barrier, then B(ks + 2) and -- at t = 0 -- the next slice's halo into the other buffer (read last
+    // by the previous slice), then the MFMAs reading A fragments at rows shifted by (kh * HP + kw).
+    static_assert(BK == 32 && NSTAGE == 3 && BM % HW_ == 0 && WM % HW_ == 0 && HW_ % 16 == 0 && FM % 2 == 0,
+                  "halo conv tile");
+    constexpr int HB_INS = BN / RPP, H_PW = (H_INS + NW - 1) / NW, BH_PW = (HB_INS + NW - 1) / NW;
+    const int h_cnt = H_INS / NW + (wave < H_INS % NW ? 1 : 0);
+    const int b_cnt = HB_INS / NW + (wave < HB_INS % NW ? 1 : 0);
+    const int pix = p.H * HW_;
+    const int bimg = m0 / pix, oh0 = (m0 - bimg * pix) / HW_;
+    unsigned hvo[H_PW], bvo[BH_PW];
+#pragma unroll
+    for (int j = 0; j < H_PW; ++j) {
+      const int row = (j * NW + wave) * RPP + lane / CPRW;
+      const int r = row / HP, c = row - r * HP;
+      const int ih = oh0 - 1 + r, iw = c - 1;
+      const bool ok = j * NW + wave < H_INS && ih >= 0 && ih < p.H && iw >= 0 && iw < HW_;
+      hvo[j] = ok ? (unsigned)(((long)(bimg * p.H + ih) * HW_ + iw) * p.lda * 2) + (unsigned)(((lane % CPRW) ^ swzk(row)) << 4)
+                  : OOB;
+    }
+#pragma unroll
+    for (int j = 0; j < BH_PW; ++j) {
+      const int row = (j * NW + wave) * RPP + lane / CPRW;
+      const int n = n0 + row;
+      bvo[j] = (j * NW + wave < HB_INS && n < p.N)
+                   ? (unsigned)((long)n * p.ldw * 2) + (unsigned)(((lane % CPRW) ^ swzk(row)) << 4) : OOB;
+    }
+    char* const hbase = smem;
+    char* const bbase = smem + 2 * HBYTES;
+    auto issue_halo = [&](int c32, int hb) {  // input channels 32 c32 .. +31 of the halo, into buffer hb
+#pragma unroll
+      for (int j = 0; j < H_PW; ++j)
+        if (j * NW + wave < H_INS) bld16(rsA, hbase + hb * HBYTES + (j * NW + wave) * 1024, hvo[j], (unsigned)(c32 * 64));
+    };
+    auto issue_b = [&](int ks) {  // global K-step ks = 9 c32 + tap: W columns ((c32 / 2) * 9 + tap) * 64 + (c32 % 2) * 32
+      const int c32 = ks / 9, tap = ks - 9 * c32;
+      const unsigned kb = (unsigned)(((c32 >> 1) * 9 + tap) * 128 + (c32 & 1) * 64);
+#pragma unroll
+      for (int j = 0; j < BH_PW; ++j)
+        if (j * NW + wave < HB_INS) bld16(rsW, bbase + (tap % 3) * BSTAGE + (j * NW + wave) * 1024, bvo[j], kb);
+    };
+    auto vm_wait = [&](int n) {  // s_waitcnt vmcnt(n) for the wave-uniform n (immediates only; smaller = safe)
+      if (n >= 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+      else if (n == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else if (n == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      else if (n == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else if (n == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      else if (n == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else if (n == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
+    static_assert((HB_INS + NW - 1) / NW + (H_INS + NW - 1) / NW <= 7, "vm_wait immediates");
+    // per-lane LDS byte offsets: A row fr of a fragment at tap column kw (swizzle of row fr + kw: the fragment's
+    // first halo row is a multiple of 8), B row fr of a fragment
+    unsigned aoff[3];
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) aoff[kw] = (unsigned)(fr * RB + ((fg ^ swzk(fr + kw)) << 4));
+    const unsigned boff = (unsigned)(fr * RB + ((fg ^ swzk(fr)) << 4));
+    const int orow_w = (wr * WM) / HW_;  // the wave's first output row within the tile
+    const int nsl = nk / 9, c_first = ks0 / 9;
+    if (nsl > 0) {
+      issue_halo(c_first, 0);
+      issue_b(ks0);
+      issue_b(ks0 + 1);
+    }
+    for (int cs = 0; cs < nsl; ++cs) {
+      const int hb = cs & 1;
+      const bool more = cs + 1 < nsl;
+      const char* hbuf = hbase + hb * HBYTES + orow_w * HP * RB;
+      auto tap_step = [&](auto tc) {
+        constexpr int t = decltype(tc)::value, kh = t / 3, kw = t % 3;
+        const int ks = cs * 9 + t;
+        int nwait = ks + 1 < nk ? b_cnt : 0;
+        if ((t == 1 || t == 2) && more) nwait += h_cnt;
+        vm_wait(nwait);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (ks + 2 < nk && !(p.diag & 1)) issue_b(ks0 + ks + 2);
+        if (t == 0 && more && !(p.diag & 1)) issue_halo(c_first + cs + 1, hb ^ 1);
+        if (p.diag & 2) return;
+        const char* sb = bbase + (t % 3) * BSTAGE + wc * WN * RB;
+        auto read_a = [&](int i) -> half8 {
+          const int i16 = 16 * i;
+          return *reinterpret_cast<const half8*>(hbuf + aoff[kw] + ((i16 / HW_ + kh) * HP + (i16 % HW_) + kw) * RB);
+        };
+        half8 bcur[FN];
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bcur[j] = *reinterpret_cast<const half8*>(sb + boff + 16 * j * RB);
+        half8 a0 = read_a(0), a1 = read_a(1);
+#pragma unroll
+        for (int g = 0; g < FM / 2; ++g) {
+          half8 n0 = a0, n1 = a1;
+          if (g + 1 < FM / 2) {
+            n0 = read_a(2 * g + 2);
+            n1 = read_a(2 * g + 3);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[2 * g][j] = mfma16x16x32(bcur[j], a0, acc[2 * g][j]);
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[2 * g + 1][j] = mfma16x16x32(bcur[j], a1, acc[2 * g + 1][j]);
+          __builtin_amdgcn_sched_barrier(0);
+          a0 = n0;
+          a1 = n1;
+        }
+      };
+      tap_step(std::integral_constant<int, 0>());
+      tap_step(std::integral_constant<int, 1>());
+      tap_step(std::integral_constant<int, 2>());
+      tap_step(std::integral_constant<int, 3>());
+      tap_step(std::integral_constant<int, 4>());
+      tap_step(std::integral_constant<int, 5>());
+      tap_step(std::integral_constant<int, 6>());
+      tap_step(std::integral_constant<int, 7>());
+      tap_step(std::integral_constant<int, 8>());
+    }
+  } else {
   // prologue: stages 0 .. NSTAGE-2
 #pragma unroll
   for (int s = 0; s < NSTAGE - 1; ++s)
     if (s < nk) issue_stage(ks0 + s, s);
 
-  const int fr = lane & 15, fg = lane >> 4;
   for (int it = 0; it < nk; ++it) {
     // wait for this K-step's tile (leave the later ones in flight), then make every wave's DMA visible
     {
@@ -578,6 +708,7 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
     }
     if (p.prio) __builtin_amdgcn_s_setprio(0);
   }
+  }  // !HALO
 
   // ---- epilogue
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -943,6 +1074,55 @@ int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s, int ks_w
     SDMOE_CHECK_LAUNCH();
   }
   return SDMOE_OK;
+}
+
+int g_halo = 1;  // knob 16: halo-tiled stride-1 3x3 convs (1, default) or the shifted-tile implicit GEMM (0)
+
+// halo conv launch: BM x 320 tiles (8 waves 2 x 4, BK 32, 3-stage B ring), K split over whole 32-channel slices when
+// the tile grid is under ~one wave of CUs
+template <int BM, int MODE>
+int launch_halo(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
+  constexpr int HW_ = halo_w(MODE);
+  const int ntiles = (p.M / BM) * (p.N / 320);
+  const int nsl = p.Cin / 32;
+  int ksplit = 1;
+  if (ws && ntiles < 200) {
+    ksplit = (256 + ntiles - 1) / ntiles;
+    if (ksplit > 8) ksplit = 8;
+    if (ksplit > nsl / 2) ksplit = nsl / 2;
+    while (ksplit > 1 && (long)ksplit * p.M * p.N > ws_floats) --ksplit;
+    if (ksplit < 1) ksplit = 1;
+  }
+  const int slc = (nsl + ksplit - 1) / ksplit;   // slices per split
+  p.ksplit = (nsl + slc - 1) / slc;
+  p.kchunk = 9 * slc;
+  p.part = p.ksplit > 1 ? ws : nullptr;
+  p.mfast = p.ksplit > 1 ? g_mfast : 0;
+  p.prio = g_prio;
+  p.diag = g_diag;
+  p.res16 = g_res16;
+  (void)HW_;
+  gemm_kernel<BM, 320, 2, 4, MODE, 3, 32><<<dim3(ntiles * p.ksplit), 512, 0, s>>>(p);
+  SDMOE_CHECK_LAUNCH();
+  if (p.ksplit > 1) {
+    long nchunk = (long)p.M * (p.N / 8);
+    int g = (int)((nchunk + 255) / 256);
+    if (g > 2048) g = 2048;
+    splitk_reduce_kernel<<<g, 256, 0, s>>>(p);
+    SDMOE_CHECK_LAUNCH();
+  }
+  return SDMOE_OK;
+}
+
+// stride-1, non-upsampling 3x3 conv without a folded shortcut on a halo tile: image widths 64 (256-row tiles = 4
+// output rows), 32 and 16 (128-row tiles), N a multiple of 320; otherwise -1 (the shifted-tile path)
+int try_halo(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
+  if (!g_halo || g_tile || p.stride != 1 || p.upsample || p.A2 || p.N % 320 || p.Cin % 32) return -1;
+  const int hw = p.H * p.Wd;
+  if (p.Wd == 64 && hw % 256 == 0) return launch_halo<256, MODE_CONVH64>(p, ws, ws_floats, s);
+  if (p.Wd == 32 && hw % 128 == 0) return launch_halo<128, MODE_CONVH32>(p, ws, ws_floats, s);
+  if (p.Wd == 16 && hw % 128 == 0) return launch_halo<128, MODE_CONVH16>(p, ws, ws_floats, s);
+  return -1;
 }
 
 // routed-GEGLU linear: BN in {160, 320} tiles only (wave tile width 80 = 40 neurons = whole experts), no split-K
@@ -1361,6 +1541,8 @@ extern "C" int sdmoe_conv3x3(const void* X, long ldx, int nimg, int H, int W, in
   if (ab >= (long)OOB || wb >= (long)OOB) return SDMOE_ESHAPE;
   p.a_bytes = (int)ab; p.w_bytes = (int)wb;
   if (upsample) return dispatch<MODE_CONV_UP>(p, workspace, workspace_floats, (hipStream_t)stream);
+  const int hs = try_halo(p, workspace, workspace_floats, (hipStream_t)stream);
+  if (hs >= 0) return hs;
   return dispatch<MODE_CONV>(p, workspace, workspace_floats, (hipStream_t)stream);
 }
 
@@ -1433,5 +1615,6 @@ extern "C" int sdmoe_tune(int knob, int value) {
   if (knob == 6 && value >= 0 && value <= 63) { g_diag = value; return SDMOE_OK; }
   if (knob == 8 && (value == 0 || value == 1)) { g_res16 = value; return SDMOE_OK; }
   if (knob == 15 && (value == 0 || value == 1 || value == 4)) { g_topk_tpw = value; return SDMOE_OK; }
+  if (knob == 16 && (value == 0 || value == 1)) { g_halo = value; return SDMOE_OK; }
   return SDMOE_EARG;
 }
