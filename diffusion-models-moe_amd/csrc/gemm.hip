@@ -59,6 +59,7 @@ struct GemmParams {
   int rows_per_batch;
   int H, Wd, Cin, OH, OW, stride, upsample;
   int ksplit, kchunk;
+  int kchunk2;  // halo conv: folded-shortcut K-steps (32 channels of A2 each) per split (kchunk = main slices per split)
   int mfast;  // tile order M-fastest (split-K grids, sdmoe_tune knob 14)
   int a_bytes, w_bytes;  // SRD num_records
   // routed-GEGLU epilogue (sdmoe_linear_geglu): W rows interleaved [value 8 | gate 8] per 8-neuron chunk, C is
@@ -153,12 +154,19 @@ SDMOE_DEV void epilogue8(const GemmParams& p, int m, int n, float (&v)[8]) {
 // WMASK: W operand masked per (row, k) by Wanda bits; KEEPW: both (the routed FFN down projection under a Wanda mask)
 // GEMM_LN / GEGLU_LN: GEMM / GEGLU with the LayerNorm of the A rows folded in (row statistics from the A tiles)
 enum { MODE_GEMM = 0, MODE_CONV = 1, MODE_CONV_UP = 2, MODE_GEGLU = 3, MODE_KEEP = 4, MODE_WMASK = 5, MODE_KEEPW = 6,
-       MODE_GEMM_LN = 7, MODE_GEGLU_LN = 8, MODE_CONVH64 = 9, MODE_CONVH32 = 10, MODE_CONVH16 = 11 };
+       MODE_GEMM_LN = 7, MODE_GEGLU_LN = 8, MODE_CONVH64 = 9, MODE_CONVH32 = 10, MODE_CONVH16 = 11,
+       MODE_CONVHUP64 = 12, MODE_CONVHUP32 = 13, MODE_CONVHUP16 = 14 };
 // halo-tiled stride-1 3x3 conv (MODE_CONVH<W>, image width W): a tile is BM / W whole output rows of one image; per
 // 32-channel slice the (BM / W + 2) x (W + 2) input halo is staged in LDS ONCE and read by all 9 taps at shifted
 // rows, instead of 9 shifted A tiles (A pieces per K-step 27/9 instead of BM / 16)
-constexpr bool mode_halo(int mode) { return mode >= MODE_CONVH64 && mode <= MODE_CONVH16; }
-constexpr int halo_w(int mode) { return mode == MODE_CONVH64 ? 64 : (mode == MODE_CONVH32 ? 32 : 16); }
+// MODE_CONVHUP<OW>: the same for the fused nearest-2x upsample conv (output width OW): the halo is the
+// (BM / OW / 2 + 2) x (OW / 2 + 2) LOW-resolution input patch; output pixel (oh, ow) at tap (kh, kw) reads input
+// ((oh + kh - 1) >> 1, (ow + kw - 1) >> 1) -- two lanes of a fragment share each input row (an LDS broadcast)
+constexpr bool mode_halo(int mode) { return mode >= MODE_CONVH64 && mode <= MODE_CONVHUP16; }
+constexpr bool mode_halo_up(int mode) { return mode >= MODE_CONVHUP64 && mode <= MODE_CONVHUP16; }
+constexpr int halo_w(int mode) {  // OUTPUT width
+  return (mode == MODE_CONVH64 || mode == MODE_CONVHUP64) ? 64 : ((mode == MODE_CONVH32 || mode == MODE_CONVHUP32) ? 32 : 16);
+}
 constexpr bool mode_akeep(int mode) { return mode == MODE_KEEP || mode == MODE_KEEPW; }
 constexpr bool mode_wmask(int mode) { return mode == MODE_WMASK || mode == MODE_KEEPW; }
 
@@ -246,9 +254,13 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
   // halo conv (MODE_CONVH*): two halo buffers of H_INS pieces (input rows BM / HW_ + 2 at a pitch of HW_ + 8 pixels: a
   // multiple of 8 rows, so a fragment's swizzle depends only on its lane and tap column) + an NSTAGE ring of B tiles
   constexpr bool HALO = mode_halo(MODE);
-  constexpr int HW_ = halo_w(MODE), HP = HW_ + 8, HR = BM / HW_;
-  constexpr int H_INS = HALO ? ((HR + 2) * HP + RPP - 1) / RPP : 0;
-  constexpr int HBYTES = H_INS * 1024, BSTAGE = BN * RB;
+  constexpr bool HUP = mode_halo_up(MODE);
+  constexpr int HW_ = halo_w(MODE), HWIN = HUP ? HW_ / 2 : HW_, HP = HWIN + 8, HR = BM / HW_;
+  constexpr int HROWS_IN = HUP ? HR / 2 + 2 : HR + 2;  // input rows of the halo
+  constexpr int H_INS = HALO ? (HROWS_IN * HP + RPP - 1) / RPP : 0;
+  // a halo buffer also holds two A2 ring slots (BM rows x 32 channels) of the folded-shortcut K-steps
+  constexpr int A2BYTES = BM * RB;
+  constexpr int HBYTES = H_INS * 1024 > 2 * A2BYTES ? H_INS * 1024 : 2 * A2BYTES, BSTAGE = BN * RB;
   constexpr int RING = HALO ? 2 * HBYTES + NSTAGE * BSTAGE : NSTAGE * STAGE;  // main-loop LDS
   constexpr int RS16 = WN + 8;
   constexpr int NPASS16 = (NW * WM * RS16 * 2 <= RING) ? 1 : (NW * (WM / 2) * RS16 * 2 <= RING) ? 2
@@ -459,25 +471,32 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
 
   const int fr = lane & 15, fg = lane >> 4;
   if constexpr (HALO) {
-    // ---- halo-tiled 3x3 conv main loop. K-step = (32-channel slice c, tap t); the 9 taps of a slice are unrolled
-    // (kh, kw, ring stage t % 3 compile-time). Per iteration: counted wait for B(ks) (and the slice's halo, always
-    // older), one barrier, then B(ks + 2) and -- at t = 0 -- the next slice's halo into the other buffer (read last
-    // by the previous slice), then the MFMAs reading A fragments at rows shifted by (kh * HP + kw).
-    static_assert(BK == 32 && NSTAGE == 3 && BM % HW_ == 0 && WM % HW_ == 0 && HW_ % 16 == 0 && FM % 2 == 0,
+    // ---- halo-tiled 3x3 conv main loop. Local K-steps: 9 per main 32-channel slice (tap t; the 9 taps unrolled: kh,
+    // kw and the B ring stage t % 3 compile-time), then the folded shortcut's K-steps (32 channels of A2 at the output
+    // pixel each). Per iteration: counted wait for K-step ks's group (its B tile, + its A2 tile on shortcut steps;
+    // the main slice's halo is always older), one barrier, then group(ks + 2) and -- at t = 0 -- the next slice's halo
+    // into the other buffer (read last by the previous slice), then the MFMAs. A2 ring slots: slot s = k2 % 3 lives
+    // in halo buffer (nsl + (s == 2)) % 2 at offset (s == 1) * A2BYTES: slots 0 / 1 are in the buffer the last main
+    // slice does not read (their loads are issued during its taps 7 / 8), slot 2 in the other one (issued after the
+    // first shortcut step's barrier).
+    static_assert(BK == 32 && NSTAGE == 3 && BM % HW_ == 0 && WM % HW_ == 0 && HW_ % 16 == 0 && FM % 2 == 0 &&
+                      (!HUP || ((WM / HW_) % 2 == 0 && HR % 2 == 0)),
                   "halo conv tile");
     constexpr int HB_INS = BN / RPP, H_PW = (H_INS + NW - 1) / NW, BH_PW = (HB_INS + NW - 1) / NW;
+    constexpr int A2_INS = BM / RPP, A2_PW = (A2_INS + NW - 1) / NW;
     const int h_cnt = H_INS / NW + (wave < H_INS % NW ? 1 : 0);
     const int b_cnt = HB_INS / NW + (wave < HB_INS % NW ? 1 : 0);
-    const int pix = p.H * HW_;
+    const int a2_cnt = p.A2 ? A2_INS / NW + (wave < A2_INS % NW ? 1 : 0) : 0;
+    const int pix = (HUP ? 2 * p.H : p.H) * HW_;  // output pixels per image
     const int bimg = m0 / pix, oh0 = (m0 - bimg * pix) / HW_;
-    unsigned hvo[H_PW], bvo[BH_PW];
+    unsigned hvo[H_PW], bvo[BH_PW], a2vo[A2_PW];
 #pragma unroll
     for (int j = 0; j < H_PW; ++j) {
       const int row = (j * NW + wave) * RPP + lane / CPRW;
       const int r = row / HP, c = row - r * HP;
-      const int ih = oh0 - 1 + r, iw = c - 1;
-      const bool ok = j * NW + wave < H_INS && ih >= 0 && ih < p.H && iw >= 0 && iw < HW_;
-      hvo[j] = ok ? (unsigned)(((long)(bimg * p.H + ih) * HW_ + iw) * p.lda * 2) + (unsigned)(((lane % CPRW) ^ swzk(row)) << 4)
+      const int ih = (HUP ? oh0 / 2 : oh0) - 1 + r, iw = c - 1;
+      const bool ok = j * NW + wave < H_INS && ih >= 0 && ih < p.H && iw >= 0 && iw < HWIN;
+      hvo[j] = ok ? (unsigned)(((long)(bimg * p.H + ih) * HWIN + iw) * p.lda * 2) + (unsigned)(((lane % CPRW) ^ swzk(row)) << 4)
                   : OOB;
     }
 #pragma unroll
@@ -487,22 +506,51 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
       bvo[j] = (j * NW + wave < HB_INS && n < p.N)
                    ? (unsigned)((long)n * p.ldw * 2) + (unsigned)(((lane % CPRW) ^ swzk(row)) << 4) : OOB;
     }
+#pragma unroll
+    for (int j = 0; j < A2_PW; ++j) {
+      const int row = (j * NW + wave) * RPP + lane / CPRW;
+      const int m = m0 + row;
+      a2vo[j] = (p.A2 && j * NW + wave < A2_INS && m < p.M)
+                    ? (unsigned)((long)m * p.lda2 * 2) + (unsigned)(((lane % CPRW) ^ swzk(row)) << 4) : OOB;
+    }
     char* const hbase = smem;
     char* const bbase = smem + 2 * HBYTES;
+    // this split's main slices [c_first, c_first + nsl) and shortcut steps [k2_first, k2_first + n2)
+    const int nsl_all = p.Cin / 32, n2_all = p.A2 ? (p.K - 9 * p.Cin) / 32 : 0;
+    const int c_first = min(nsl_all, split * p.kchunk), nsl = min(nsl_all, c_first + p.kchunk) - c_first;
+    const int k2_first = min(n2_all, split * p.kchunk2), n2 = min(n2_all, k2_first + p.kchunk2) - k2_first;
+    const int nkl = 9 * nsl + n2;
     auto issue_halo = [&](int c32, int hb) {  // input channels 32 c32 .. +31 of the halo, into buffer hb
 #pragma unroll
       for (int j = 0; j < H_PW; ++j)
         if (j * NW + wave < H_INS) bld16(rsA, hbase + hb * HBYTES + (j * NW + wave) * 1024, hvo[j], (unsigned)(c32 * 64));
     };
-    auto issue_b = [&](int ks) {  // global K-step ks = 9 c32 + tap: W columns ((c32 / 2) * 9 + tap) * 64 + (c32 % 2) * 32
-      const int c32 = ks / 9, tap = ks - 9 * c32;
-      const unsigned kb = (unsigned)(((c32 >> 1) * 9 + tap) * 128 + (c32 & 1) * 64);
+    auto issue_group = [&](int ks) {  // local K-step ks: its B tile (+ A2 tile on a shortcut step) into ring slot ks % 3
+      unsigned kb;
+      const int slot = ks % 3;
+      if (ks < 9 * nsl) {  // W columns ((c32 / 2) * 9 + tap) * 64 + (c32 % 2) * 32
+        const int c32 = c_first + ks / 9, tap = ks % 9;
+        kb = (unsigned)(((c32 >> 1) * 9 + tap) * 128 + (c32 & 1) * 64);
+      } else {  // W columns 9 Cin + 32 k2
+        const int k2 = k2_first + ks - 9 * nsl;
+        kb = (unsigned)(18 * p.Cin + 64 * k2);
+        char* const a2s = hbase + ((nsl + (slot == 2 ? 1 : 0)) & 1) * HBYTES + (slot == 1 ? A2BYTES : 0);
+#pragma unroll
+        for (int j = 0; j < A2_PW; ++j)
+          if (j * NW + wave < A2_INS) bld16(rsA2, a2s + (j * NW + wave) * 1024, a2vo[j], (unsigned)(64 * k2));
+      }
 #pragma unroll
       for (int j = 0; j < BH_PW; ++j)
-        if (j * NW + wave < HB_INS) bld16(rsW, bbase + (tap % 3) * BSTAGE + (j * NW + wave) * 1024, bvo[j], kb);
+        if (j * NW + wave < HB_INS) bld16(rsW, bbase + slot * BSTAGE + (j * NW + wave) * 1024, bvo[j], kb);
     };
+    auto group_cnt = [&](int ks) { return ks < 9 * nsl ? b_cnt : b_cnt + a2_cnt; };
     auto vm_wait = [&](int n) {  // s_waitcnt vmcnt(n) for the wave-uniform n (immediates only; smaller = safe)
-      if (n >= 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+      if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      else if (n == 11) asm volatile("s_waitcnt vmcnt(11)" ::: "memory");
+      else if (n == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+      else if (n == 9) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+      else if (n == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (n == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
       else if (n == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
       else if (n == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
       else if (n == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -511,60 +559,69 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
       else if (n == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     };
-    static_assert((HB_INS + NW - 1) / NW + (H_INS + NW - 1) / NW <= 7, "vm_wait immediates");
-    // per-lane LDS byte offsets: A row fr of a fragment at tap column kw (swizzle of row fr + kw: the fragment's
-    // first halo row is a multiple of 8), B row fr of a fragment
+    // per-lane LDS byte offsets: A row fr of a halo fragment at tap column kw (swizzle of row fr + kw: the fragment's
+    // first halo row is a multiple of 8), row fr of an aligned B / A2 fragment
     unsigned aoff[3];
 #pragma unroll
-    for (int kw = 0; kw < 3; ++kw) aoff[kw] = (unsigned)(fr * RB + ((fg ^ swzk(fr + kw)) << 4));
+    for (int kw = 0; kw < 3; ++kw) {  // upsample: lane fr reads input column offset (fr + kw + 1) >> 1
+      const int rr = HUP ? (fr + kw + 1) >> 1 : fr + kw;
+      aoff[kw] = (unsigned)((HUP ? rr : fr) * RB + ((fg ^ swzk(rr)) << 4));
+    }
     const unsigned boff = (unsigned)(fr * RB + ((fg ^ swzk(fr)) << 4));
     const int orow_w = (wr * WM) / HW_;  // the wave's first output row within the tile
-    const int nsl = nk / 9, c_first = ks0 / 9;
-    if (nsl > 0) {
-      issue_halo(c_first, 0);
-      issue_b(ks0);
-      issue_b(ks0 + 1);
+    // MFMAs of one K-step: A fragment i from a_at(i), B fragments from sb
+    auto mfma_step = [&](const char* sb, auto&& a_at) {
+      half8 bcur[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bcur[j] = *reinterpret_cast<const half8*>(sb + boff + 16 * j * RB);
+      half8 a0 = a_at(0), a1 = a_at(1);
+#pragma unroll
+      for (int g = 0; g < FM / 2; ++g) {
+        half8 n0 = a0, n1 = a1;
+        if (g + 1 < FM / 2) {
+          n0 = a_at(2 * g + 2);
+          n1 = a_at(2 * g + 3);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[2 * g][j] = mfma16x16x32(bcur[j], a0, acc[2 * g][j]);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[2 * g + 1][j] = mfma16x16x32(bcur[j], a1, acc[2 * g + 1][j]);
+        __builtin_amdgcn_sched_barrier(0);
+        a0 = n0;
+        a1 = n1;
+      }
+    };
+    if (nkl > 0) {
+      if (nsl > 0) issue_halo(c_first, 0);
+      issue_group(0);
+      if (nkl > 1) issue_group(1);
     }
     for (int cs = 0; cs < nsl; ++cs) {
       const int hb = cs & 1;
       const bool more = cs + 1 < nsl;
-      const char* hbuf = hbase + hb * HBYTES + orow_w * HP * RB;
+      const char* hbuf = hbase + hb * HBYTES + (HUP ? orow_w / 2 : orow_w) * HP * RB;
       auto tap_step = [&](auto tc) {
         constexpr int t = decltype(tc)::value, kh = t / 3, kw = t % 3;
         const int ks = cs * 9 + t;
-        int nwait = ks + 1 < nk ? b_cnt : 0;
+        // younger than group(ks) (issued at iteration ks - 2): the halo issued at iteration ks - 2 (t == 2) or
+        // ks - 1 (t == 1), and group(ks + 1)
+        int nwait = ks + 1 < nkl ? group_cnt(ks + 1) : 0;
         if ((t == 1 || t == 2) && more) nwait += h_cnt;
         vm_wait(nwait);
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (ks + 2 < nk && !(p.diag & 1)) issue_b(ks0 + ks + 2);
+        if (ks + 2 < nkl && !(p.diag & 1)) issue_group(ks + 2);
         if (t == 0 && more && !(p.diag & 1)) issue_halo(c_first + cs + 1, hb ^ 1);
         if (p.diag & 2) return;
-        const char* sb = bbase + (t % 3) * BSTAGE + wc * WN * RB;
-        auto read_a = [&](int i) -> half8 {
+        mfma_step(bbase + (t % 3) * BSTAGE + wc * WN * RB, [&](int i) -> half8 {
           const int i16 = 16 * i;
-          return *reinterpret_cast<const half8*>(hbuf + aoff[kw] + ((i16 / HW_ + kh) * HP + (i16 % HW_) + kw) * RB);
-        };
-        half8 bcur[FN];
-#pragma unroll
-        for (int j = 0; j < FN; ++j) bcur[j] = *reinterpret_cast<const half8*>(sb + boff + 16 * j * RB);
-        half8 a0 = read_a(0), a1 = read_a(1);
-#pragma unroll
-        for (int g = 0; g < FM / 2; ++g) {
-          half8 n0 = a0, n1 = a1;
-          if (g + 1 < FM / 2) {
-            n0 = read_a(2 * g + 2);
-            n1 = read_a(2 * g + 3);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int j = 0; j < FN; ++j) acc[2 * g][j] = mfma16x16x32(bcur[j], a0, acc[2 * g][j]);
-#pragma unroll
-          for (int j = 0; j < FN; ++j) acc[2 * g + 1][j] = mfma16x16x32(bcur[j], a1, acc[2 * g + 1][j]);
-          __builtin_amdgcn_sched_barrier(0);
-          a0 = n0;
-          a1 = n1;
-        }
+          if constexpr (HUP)  // input row ((orow + kh - 1) >> 1) - (oh0 / 2 - 1), column (ocol0 / 2) + lane part
+            return *reinterpret_cast<const half8*>(hbuf + aoff[kw] +
+                                                   (((((i16 / HW_) + kh - 1) >> 1) + 1) * HP + (i16 % HW_) / 2) * RB);
+          else
+            return *reinterpret_cast<const half8*>(hbuf + aoff[kw] + ((i16 / HW_ + kh) * HP + (i16 % HW_) + kw) * RB);
+        });
       };
       tap_step(std::integral_constant<int, 0>());
       tap_step(std::integral_constant<int, 1>());
@@ -575,6 +632,18 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
       tap_step(std::integral_constant<int, 6>());
       tap_step(std::integral_constant<int, 7>());
       tap_step(std::integral_constant<int, 8>());
+    }
+    for (int k2l = 0; k2l < n2; ++k2l) {  // folded shortcut K-steps
+      const int ks = 9 * nsl + k2l, slot = ks % 3;
+      vm_wait(ks + 1 < nkl ? group_cnt(ks + 1) : 0);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (ks + 2 < nkl && !(p.diag & 1)) issue_group(ks + 2);
+      if (p.diag & 2) continue;
+      const char* a2s = hbase + ((nsl + (slot == 2 ? 1 : 0)) & 1) * HBYTES + (slot == 1 ? A2BYTES : 0) + wr * WM * RB;
+      mfma_step(bbase + slot * BSTAGE + wc * WN * RB, [&](int i) -> half8 {
+        return *reinterpret_cast<const half8*>(a2s + boff + 16 * i * RB);
+      });
     }
   } else {
   // prologue: stages 0 .. NSTAGE-2
@@ -1093,9 +1162,10 @@ int launch_halo(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
     while (ksplit > 1 && (long)ksplit * p.M * p.N > ws_floats) --ksplit;
     if (ksplit < 1) ksplit = 1;
   }
-  const int slc = (nsl + ksplit - 1) / ksplit;   // slices per split
+  const int slc = (nsl + ksplit - 1) / ksplit;   // main slices per split
   p.ksplit = (nsl + slc - 1) / slc;
-  p.kchunk = 9 * slc;
+  p.kchunk = slc;
+  p.kchunk2 = p.A2 ? ((p.K - 9 * p.Cin) / 32 + p.ksplit - 1) / p.ksplit : 0;  // shortcut steps per split
   p.part = p.ksplit > 1 ? ws : nullptr;
   p.mfast = p.ksplit > 1 ? g_mfast : 0;
   p.prio = g_prio;
@@ -1114,10 +1184,18 @@ int launch_halo(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
   return SDMOE_OK;
 }
 
-// stride-1, non-upsampling 3x3 conv without a folded shortcut on a halo tile: image widths 64 (256-row tiles = 4
+// stride-1, non-upsampling 3x3 conv (+ folded shortcut) on a halo tile: image widths 64 (256-row tiles = 4
 // output rows), 32 and 16 (128-row tiles), N a multiple of 320; otherwise -1 (the shifted-tile path)
 int try_halo(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
-  if (!g_halo || g_tile || p.stride != 1 || p.upsample || p.A2 || p.N % 320 || p.Cin % 32) return -1;
+  if (!g_halo || g_tile || p.stride != 1 || p.N % 320 || p.Cin % 32 || (p.K - 9 * p.Cin) % 32) return -1;
+  if (p.upsample) {  // output width 2 W, output rows per image 2 H
+    if (p.A2) return -1;
+    const int ohw = 4 * p.H * p.Wd;
+    if (p.Wd == 32 && ohw % 256 == 0) return launch_halo<256, MODE_CONVHUP64>(p, ws, ws_floats, s);
+    if (p.Wd == 16 && ohw % 128 == 0) return launch_halo<128, MODE_CONVHUP32>(p, ws, ws_floats, s);
+    if (p.Wd == 8 && ohw % 128 == 0) return launch_halo<128, MODE_CONVHUP16>(p, ws, ws_floats, s);
+    return -1;
+  }
   const int hw = p.H * p.Wd;
   if (p.Wd == 64 && hw % 256 == 0) return launch_halo<256, MODE_CONVH64>(p, ws, ws_floats, s);
   if (p.Wd == 32 && hw % 128 == 0) return launch_halo<128, MODE_CONVH32>(p, ws, ws_floats, s);
@@ -1540,9 +1618,9 @@ extern "C" int sdmoe_conv3x3(const void* X, long ldx, int nimg, int H, int W, in
   const long ab = ((long)nimg * H * W - 1) * ldx * 2 + (long)Cin * 2, wb = (long)Cout * 9 * Cin * 2;
   if (ab >= (long)OOB || wb >= (long)OOB) return SDMOE_ESHAPE;
   p.a_bytes = (int)ab; p.w_bytes = (int)wb;
-  if (upsample) return dispatch<MODE_CONV_UP>(p, workspace, workspace_floats, (hipStream_t)stream);
   const int hs = try_halo(p, workspace, workspace_floats, (hipStream_t)stream);
   if (hs >= 0) return hs;
+  if (upsample) return dispatch<MODE_CONV_UP>(p, workspace, workspace_floats, (hipStream_t)stream);
   return dispatch<MODE_CONV>(p, workspace, workspace_floats, (hipStream_t)stream);
 }
 
@@ -1565,6 +1643,8 @@ extern "C" int sdmoe_conv3x3_sc(const void* X, long ldx, int nimg, int H, int W,
   const long a2b = ((long)nimg * H * W - 1) * ldx2 * 2 + (long)Cin2 * 2;
   if (ab >= (long)OOB || wb >= (long)OOB || a2b >= (long)OOB) return SDMOE_ESHAPE;
   p.a_bytes = (int)ab; p.w_bytes = (int)wb; p.a2_bytes = (int)a2b;
+  const int hs = try_halo(p, workspace, workspace_floats, (hipStream_t)stream);
+  if (hs >= 0) return hs;
   return dispatch<MODE_CONV>(p, workspace, workspace_floats, (hipStream_t)stream);
 }
 

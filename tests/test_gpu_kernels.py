@@ -396,23 +396,30 @@ def test_conv3x3_full_size_tiles(tile, stages):
     _with_tune([(1, tile), (0, stages)], run)
 
 
-@pytest.mark.parametrize("H,Cin,Cout,nimg", [(64, 320, 320, 16), (64, 960, 320, 2), (64, 64, 320, 2), (32, 640, 640, 16),
-                                             (32, 1280, 640, 4), (32, 320, 640, 2), (16, 1280, 1280, 16),
-                                             (16, 2560, 1280, 2), (16, 640, 1280, 3)])
-def test_conv3x3_halo_tiles(H, Cin, Cout, nimg):
-    """Halo-tiled stride-1 convs (MODE_CONVH64/32/16, sdmoe_tune knob 16 = 1, default): the (rows + 2) x (W + 2) input
-    halo of each 32-channel slice staged once for the 9 taps, incl. image borders, K split over slices (small grids:
-    nimg 2-4) and the time-embedding column add + residual epilogue; vs torch fp32 and vs the shifted-tile path
-    (knob 16 = 0) within the same tolerance (the K order differs: 32- vs 64-channel slices)."""
+@pytest.mark.parametrize("H,Cin,Cout,nimg,up", [(64, 320, 320, 16, False), (64, 960, 320, 2, False),
+                                                (64, 64, 320, 2, False), (32, 640, 640, 16, False),
+                                                (32, 1280, 640, 4, False), (32, 320, 640, 2, False),
+                                                (16, 1280, 1280, 16, False), (16, 2560, 1280, 2, False),
+                                                (16, 640, 1280, 3, False), (32, 640, 640, 16, True),
+                                                (32, 640, 640, 2, True), (16, 1280, 1280, 16, True),
+                                                (8, 1280, 1280, 3, True)])
+def test_conv3x3_halo_tiles(H, Cin, Cout, nimg, up):
+    """Halo-tiled stride-1 convs (MODE_CONVH64/32/16 and the 2x-upsample MODE_CONVHUP64/32/16, sdmoe_tune knob 16 = 1,
+    default): the input halo of each 32-channel slice staged once for the 9 taps, incl. image borders, K split over
+    slices (small grids: nimg 2-4) and the time-embedding column add + residual epilogue; vs torch fp32 and vs the
+    shifted-tile path (knob 16 = 0) within the same tolerance (the K order differs: 32- vs 64-channel slices)."""
+    OH = 2 * H if up else H
     x = rnd(nimg * H * H, Cin, seed=H + Cin)
     w, b = rnd(Cout, 3, 3, Cin, scale=(9 * Cin) ** -0.5, seed=H + Cout), rnd(Cout, scale=0.1, seed=3)
-    temb, res = rnd(nimg, Cout, seed=4), rnd(nimg * H * H, Cout, seed=5)
-    ref = conv_ref(x, nimg, H, H, w, b) + temb.float().repeat_interleave(H * H, 0) + res.float()
+    temb, res = rnd(nimg, Cout, seed=4), rnd(nimg * OH * OH, Cout, seed=5)
+    ref = conv_ref(x, nimg, H, H, w, b, 1, up)
+    if not up:
+        ref = ref + temb.float().repeat_interleave(H * H, 0) + res.float()
     wc = ops.conv_weight(w)
     outs = []
+    kw = {} if up else dict(coladd=temb, coladd_bstride=Cout, residual=res)
     for halo in (1, 0):
-        _with_tune([(16, halo)], lambda: outs.append(ops.conv3x3(x, nimg, H, H, wc, b, coladd=temb, coladd_bstride=Cout,
-                                                                 residual=res)))
+        _with_tune([(16, halo)], lambda: outs.append(ops.conv3x3(x, nimg, H, H, wc, b, upsample=up, **kw)))
     close(outs[0], ref)
     close(outs[1], ref)
     close(outs[0], outs[1].float())
