@@ -155,7 +155,9 @@ SDMOE_DEV void epilogue8(const GemmParams& p, int m, int n, float (&v)[8]) {
 // GEMM_LN / GEGLU_LN: GEMM / GEGLU with the LayerNorm of the A rows folded in (row statistics from the A tiles)
 enum { MODE_GEMM = 0, MODE_CONV = 1, MODE_CONV_UP = 2, MODE_GEGLU = 3, MODE_KEEP = 4, MODE_WMASK = 5, MODE_KEEPW = 6,
        MODE_GEMM_LN = 7, MODE_GEGLU_LN = 8, MODE_CONVH64 = 9, MODE_CONVH32 = 10, MODE_CONVH16 = 11,
-       MODE_CONVHUP64 = 12, MODE_CONVHUP32 = 13, MODE_CONVHUP16 = 14 };
+       MODE_CONVHUP64 = 12, MODE_CONVHUP32 = 13, MODE_CONVHUP16 = 14, MODE_GEGLU_GT = 15 };
+// MODE_GEGLU_GT: the routed GEGLU with act = GELU from the registered table (its own instantiation: a third epilogue
+// variant inside MODE_GEGLU pushed the 256x320 kernel past 256 VGPRs into scratch, 115 -> 494 us)
 // halo-tiled stride-1 3x3 conv (MODE_CONVH<W>, image width W): a tile is BM / W whole output rows of one image; per
 // 32-channel slice the (BM / W + 2) x (W + 2) input halo is staged in LDS ONCE and read by all 9 taps at shifted
 // rows, instead of 9 shifted A tiles (A pieces per K-step 27/9 instead of BM / 16)
@@ -228,7 +230,7 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
   constexpr int RPP = 1024 / RB;                 // rows per 1-KiB LDS-DMA piece
   auto swzk = [](int row) { return (row >> 1) & (CPRW - 1); };  // conflict-free b128 fragment reads
   constexpr bool CONV = MODE == MODE_CONV || MODE == MODE_CONV_UP;
-  constexpr bool GEGLU = MODE == MODE_GEGLU || MODE == MODE_GEGLU_LN;
+  constexpr bool GEGLU = MODE == MODE_GEGLU || MODE == MODE_GEGLU_LN || MODE == MODE_GEGLU_GT;
   constexpr bool LN = MODE == MODE_GEMM_LN || MODE == MODE_GEGLU_LN;
   constexpr bool AKEEP = mode_akeep(MODE), WKEEP = mode_wmask(MODE);
   constexpr bool KEEP = AKEEP || WKEEP;
@@ -447,9 +449,10 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
   // at step nk - NSTAGE, or never), when a stage holds it; otherwise after the main loop, behind the staging area
   constexpr int TAB_BYTES = GELU_TAB_N * 2;
   constexpr int G_STAGING = NW * 2 * (16 * (FM % 2 == 0 ? 2 : 1)) * (WN / 2) * 2 + NW * WN * 4;  // GEGLU epilogue
-  constexpr bool TAB_PREFETCH = GEGLU && STAGE >= TAB_BYTES && G_STAGING <= STAGE;
+  constexpr bool TAB_PREFETCH = MODE == MODE_GEGLU_GT && STAGE >= TAB_BYTES && G_STAGING <= STAGE;
   constexpr int TAB_LATE_OFF = ((G_STAGING + 1023) / 1024) * 1024;
-  constexpr bool TAB_OK = GEGLU && (TAB_PREFETCH || TAB_LATE_OFF + TAB_BYTES <= SMEM1);  // else apply_act's erfc
+  constexpr bool TAB_OK = MODE == MODE_GEGLU_GT && (TAB_PREFETCH || TAB_LATE_OFF + TAB_BYTES <= SMEM1);
+  static_assert(MODE != MODE_GEGLU_GT || TAB_OK, "GELU table must fit this tile's LDS");
   auto issue_gelu_tab = [&](char* dst) {
     const __amdgpu_buffer_rsrc_t rsT = __builtin_amdgcn_make_buffer_rsrc((void*)p.gelu_tab, (short)0, TAB_BYTES, 0x00020000);
 #pragma unroll
@@ -667,7 +670,7 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (it + NSTAGE - 1 < nk && !(p.diag & 1)) issue_stage(ks0 + it + NSTAGE - 1, (it + NSTAGE - 1) % NSTAGE);
-    else if (TAB_PREFETCH && it == nk - 1 && p.gelu_tab && p.act == ACT_GELU) issue_gelu_tab(smem + (nk % NSTAGE) * STAGE + STAGE - TAB_BYTES);
+    else if (TAB_PREFETCH && it == nk - 1) issue_gelu_tab(smem + (nk % NSTAGE) * STAGE + STAGE - TAB_BYTES);
 
     const char* sa = smem + (it % NSTAGE) * STAGE;
     const char* sbm = sa + BM * BK * 2;
@@ -925,6 +928,11 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
     return;
   }
   if constexpr (GEGLU) {
+    // lane-derived epilogue values from an opaque copy of the lane id: nothing of this epilogue can be hoisted
+    // above the main loop (hoisted addresses kept the table-GELU variant's K loop in scratch)
+    int lane_o = lane;
+    asm volatile("" : "+v"(lane_o));
+    const int fr_e = lane_o & 15, fg_e = lane_o >> 4;
     // Routed GEGLU on the swapped fragments, value and gate paired in registers: lane (fr, fg) holds columns
     // 16 j + 4 fg .. +3 of row 16 i + fr, i.e. values of 4 neurons (fg 0/1) or their gates (fg 2/3, lane + 32).
     // Two v_permlane32_swap per fragment leave lane (fr, fg) with value and gate of neurons 8 j + nsel, +1
@@ -943,7 +951,7 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
     // staging base: with the GELU table prefetched into ring stage nk % NSTAGE, the stage of the last K-step (free
     // since the barrier above) holds the staging; otherwise offset 0 and a late-loaded table behind the staging
     static_assert(GST + NW * WN * 4 == G_STAGING, "GEGLU staging size");
-    const bool gtab = TAB_OK && p.act == ACT_GELU && p.gelu_tab != nullptr;
+    constexpr bool gtab = TAB_OK;  // MODE_GEGLU_GT: launched only with a registered table and act = GELU
     char* const sbase = (TAB_PREFETCH && gtab) ? smem + ((nk - 1) % NSTAGE) * STAGE : smem;
     const half_t* const tab = reinterpret_cast<const half_t*>(
         TAB_PREFETCH ? smem + (nk % NSTAGE) * STAGE + STAGE - TAB_BYTES : smem + TAB_LATE_OFF);
@@ -957,20 +965,21 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
     half_t* sp = reinterpret_cast<half_t*>(sbase) + wave * 2 * RG * NH;  // products [RG][NH]
     half_t* sg = sp + RG * NH;                                           // activated gates [RG][NH]
     float* gbias = reinterpret_cast<float*>(sbase + GST) + wave * WN;    // this wave's WN bias values (fp32)
-    for (int c = lane; c < WN; c += 64) gbias[c] = LN ? p.ln_bias[nw + c] : (float)p.bias[nw + c];
+    for (int c = lane_o; c < WN; c += 64) gbias[c] = LN ? p.ln_bias[nw + c] : (float)p.bias[nw + c];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const int nsel = (fg & 1) * 4 + (fg >> 1) * 2;
+    const int nsel = (fg_e & 1) * 4 + (fg_e >> 1) * 2;
     constexpr int CPO = NH / 8, RPI = 64 / CPO;  // copy-out: 16-B chunks per staged row, rows per 64-lane round
-    const int lr = lane / CPO, lc = lane - (lane / CPO) * CPO;
+    const int lr = lane_o / CPO, lc = lane_o - (lane_o / CPO) * CPO;
     half_t* const cout = p.C + (long)(mw + lr) * p.ldc + nw / 2 + 8 * lc;
     // this lane's bias pairs in every fragment (value cols 16 j + nsel, +1; gate cols +8), hoisted out of the rows
+    // (the table GELU's epilogue reads them from LDS per fragment instead: its temporaries need those 20 VGPRs)
     float2v bvv[FN], bgg[FN];
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      bvv[j] = *reinterpret_cast<const float2v*>(gbias + 16 * j + nsel);
-      bgg[j] = *reinterpret_cast<const float2v*>(gbias + 16 * j + 8 + nsel);
+      bvv[j] = gtab ? (float2v){0.f, 0.f} : *reinterpret_cast<const float2v*>(gbias + 16 * j + nsel);
+      bgg[j] = gtab ? (float2v){0.f, 0.f} : *reinterpret_cast<const float2v*>(gbias + 16 * j + 8 + nsel);
     }
     auto stage_pass = [&](int h, auto act_tag) {
       constexpr int ACTK = decltype(act_tag)::value;  // 0: ReLU, 1: GELU from the LDS table, 2: apply_act
@@ -980,7 +989,7 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
         const int i = h * FPP + ii;
         float la = 0.f, lc = 0.f;
         if constexpr (LN) {
-          const int rl = wr * WM + 16 * i + fr;
+          const int rl = wr * WM + 16 * i + fr_e;
           la = ln_row[2 * rl];
           lc = ln_row[2 * rl + 1];
         }
@@ -988,28 +997,32 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
         for (int j = 0; j < FN; ++j) {
           float4v v = acc[i][j];
           if constexpr (LN) {  // rstd * (acc - mean * wsum); ln_bias is the bias below
-            const float4v ws = *reinterpret_cast<const float4v*>(ln_col + wc * WN + 16 * j + 4 * fg);
+            const float4v ws = *reinterpret_cast<const float4v*>(ln_col + wc * WN + 16 * j + 4 * fg_e);
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = __builtin_fmaf(la, v[r], lc * ws[r]);
           }
           const auto s02 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[0]), __float_as_uint(v[2]), false, false);
           const auto s13 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[1]), __float_as_uint(v[3]), false, false);
-          const h2 yv = {(half_t)(__uint_as_float(s02[0]) + bvv[j][0]), (half_t)(__uint_as_float(s13[0]) + bvv[j][1])};
-          const h2 yg = {(half_t)(__uint_as_float(s02[1]) + bgg[j][0]), (half_t)(__uint_as_float(s13[1]) + bgg[j][1])};
+          const float2v bv = ACTK == 1 ? *reinterpret_cast<const float2v*>(gbias + 16 * j + nsel) : bvv[j];
+          const float2v bg = ACTK == 1 ? *reinterpret_cast<const float2v*>(gbias + 16 * j + 8 + nsel) : bgg[j];
+          const h2 yv = {(half_t)(__uint_as_float(s02[0]) + bv[0]), (half_t)(__uint_as_float(s13[0]) + bv[1])};
+          const h2 yg = {(half_t)(__uint_as_float(s02[1]) + bg[0]), (half_t)(__uint_as_float(s13[1]) + bg[1])};
           h2 ga;
           if constexpr (RELU) ga = __builtin_elementwise_max(yg, (h2){(half_t)0.f, (half_t)0.f});
           else if constexpr (ACTK == 1) ga = (h2){gelu_tab_h(yg[0], tab), gelu_tab_h(yg[1], tab)};
           else ga = (h2){(half_t)apply_act((float)yg[0], p.act), (half_t)apply_act((float)yg[1], p.act)};
-          const int off = (16 * ii + fr) * NH + 8 * j + nsel;
+          const int off = (16 * ii + fr_e) * NH + 8 * j + nsel;
           *reinterpret_cast<h2*>(sp + off) = yv * ga;  // fp16 x fp16 is exact in fp32: rounds like the unfused path
           *reinterpret_cast<h2*>(sg + off) = ga;
+          // the table GELU's temporaries: one fragment at a time (interleaving all FN pushed 256x320 into scratch)
+          if constexpr (ACTK == 1) __builtin_amdgcn_sched_barrier(0);
         }
       }
     };
 #pragma unroll
     for (int h = 0; h < FM / FPP; ++h) {
-      if (p.act == ACT_RELU) stage_pass(h, std::integral_constant<int, 0>());
-      else if (gtab) stage_pass(h, std::integral_constant<int, 1>());
+      if constexpr (gtab) stage_pass(h, std::integral_constant<int, 1>());
+      else if (p.act == ACT_RELU) stage_pass(h, std::integral_constant<int, 0>());
       else stage_pass(h, std::integral_constant<int, 2>());
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -1028,14 +1041,14 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
       }
       if (p.score) {
         switch (p.esize) {
-          case 20: expert_sums<20, NH, RG>(p, sg, mr0, nw, lane); break;
-          case 10: expert_sums<10, NH, RG>(p, sg, mr0, nw, lane); break;
-          case 40: expert_sums<40, NH, RG>(p, sg, mr0, nw, lane); break;
-          case 8: expert_sums<8, NH, RG>(p, sg, mr0, nw, lane); break;
-          case 5: expert_sums<5, NH, RG>(p, sg, mr0, nw, lane); break;
-          case 4: expert_sums<4, NH, RG>(p, sg, mr0, nw, lane); break;
-          case 2: expert_sums<2, NH, RG>(p, sg, mr0, nw, lane); break;
-          default: expert_sums<1, NH, RG>(p, sg, mr0, nw, lane); break;
+          case 20: expert_sums<20, NH, RG>(p, sg, mr0, nw, lane_o); break;
+          case 10: expert_sums<10, NH, RG>(p, sg, mr0, nw, lane_o); break;
+          case 40: expert_sums<40, NH, RG>(p, sg, mr0, nw, lane_o); break;
+          case 8: expert_sums<8, NH, RG>(p, sg, mr0, nw, lane_o); break;
+          case 5: expert_sums<5, NH, RG>(p, sg, mr0, nw, lane_o); break;
+          case 4: expert_sums<4, NH, RG>(p, sg, mr0, nw, lane_o); break;
+          case 2: expert_sums<2, NH, RG>(p, sg, mr0, nw, lane_o); break;
+          default: expert_sums<1, NH, RG>(p, sg, mr0, nw, lane_o); break;
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1145,7 +1158,10 @@ int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s, int ks_w
   return SDMOE_OK;
 }
 
-int g_halo = 1;  // knob 16: halo-tiled stride-1 3x3 convs (1, default) or the shifted-tile implicit GEMM (0)
+// knob 16: halo-tiled stride-1 3x3 convs: 1 (default) = on the 256-row tiles (64-wide outputs: the 64x64 level and the
+// 32 -> 64 upsample conv) where they measured faster; 2 = also the 128-row tiles (32- / 16-wide outputs: 9-12 %
+// slower than the shifted-tile path there, their 32-deep K-steps carry half the MFMAs per barrier); 0 = off
+int g_halo = 1;
 
 // halo conv launch: BM x 320 tiles (8 waves 2 x 4, BK 32, 3-stage B ring), K split over whole 32-channel slices when
 // the tile grid is under ~one wave of CUs
@@ -1192,12 +1208,14 @@ int try_halo(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
     if (p.A2) return -1;
     const int ohw = 4 * p.H * p.Wd;
     if (p.Wd == 32 && ohw % 256 == 0) return launch_halo<256, MODE_CONVHUP64>(p, ws, ws_floats, s);
+    if (g_halo < 2) return -1;
     if (p.Wd == 16 && ohw % 128 == 0) return launch_halo<128, MODE_CONVHUP32>(p, ws, ws_floats, s);
     if (p.Wd == 8 && ohw % 128 == 0) return launch_halo<128, MODE_CONVHUP16>(p, ws, ws_floats, s);
     return -1;
   }
   const int hw = p.H * p.Wd;
   if (p.Wd == 64 && hw % 256 == 0) return launch_halo<256, MODE_CONVH64>(p, ws, ws_floats, s);
+  if (g_halo < 2) return -1;
   if (p.Wd == 32 && hw % 128 == 0) return launch_halo<128, MODE_CONVH32>(p, ws, ws_floats, s);
   if (p.Wd == 16 && hw % 128 == 0) return launch_halo<128, MODE_CONVH16>(p, ws, ws_floats, s);
   return -1;
@@ -1210,7 +1228,12 @@ int dispatch_geglu(const GemmParams& p, hipStream_t s) {
   const int nt160_128 = ((p.M + 127) / 128) * (p.N / 160);
   if (g_tile == 1) return launch_tile<128, 160, 2, 2, MODE>(p, nullptr, 0, s);
   if (g_tile == 4) return launch_tile<256, 160, 4, 2, MODE>(p, nullptr, 0, s);
-  if (g_tile == 7) return launch_tile<128, 160, 4, 2, MODE>(p, nullptr, 0, s);  // sweep: two workgroups per CU
+  if constexpr (MODE != MODE_GEGLU_GT)  // (no room for the GELU table behind that tile's staging)
+    if (g_tile == 7) return launch_tile<128, 160, 4, 2, MODE>(p, nullptr, 0, s);  // sweep: two workgroups per CU
+  if (MODE == MODE_GEGLU_GT && g_tile == 0 && p.N % 320 == 0 && nt320 >= 240)
+    // the table-GELU epilogue does not fit 256x320's registers next to the 160 accumulators (scratch in the K loop):
+    // the same rows on 256x160 tiles, 8 waves 4 x 2 (wave tile 64 x 80)
+    return launch_tile<256, 160, 4, 2, MODE>(p, nullptr, 0, s);
   if (p.N % 320 == 0 && nt320 >= 240) {
     // 2x4 waves (wave tile 128 rows x 40 neurons): with the row-fastest epilogue its 32-row staging passes are
     // conflict-free (4x2's 16-row passes are not: two 16-lane b128 groups mix column pairs); 174.6 vs 181.2 us at
@@ -1546,6 +1569,7 @@ extern "C" int sdmoe_linear_geglu(const void* A, long lda, const void* W, long l
   const long ab = ((long)(M - 1) * lda + K) * 2, wb = ((long)(2 * F - 1) * ldw + K) * 2;
   if (ab >= (long)OOB || wb >= (long)OOB) return SDMOE_ESHAPE;
   p.a_bytes = (int)ab; p.w_bytes = (int)wb;
+  if (p.gelu_tab) return dispatch_geglu<MODE_GEGLU_GT>(p, (hipStream_t)stream);
   return dispatch_geglu<MODE_GEGLU>(p, (hipStream_t)stream);
 }
 
@@ -1589,8 +1613,7 @@ extern "C" int sdmoe_linear_geglu_ln(const void* A, long lda, const void* W, lon
   p.C = (half_t*)P; p.ldc = ldp;
   p.M = M; p.N = 2 * F; p.K = K; p.act = act; p.rows_per_batch = 1;
   p.score = (half_t*)score; p.ld_score = ld_score; p.esize = esize;
-  p.ln_wsum = wsum; p.ln_bias = bias_f; p.ln_eps = eps;
-  if (act == ACT_GELU) p.gelu_tab = sdmoe_gelu_tab_current();
+  p.ln_wsum = wsum; p.ln_bias = bias_f; p.ln_eps = eps;  // (GELU from erfc here: the LN variant has no table form)
   const long ab = ((long)(M - 1) * lda + K) * 2, wb = ((long)(2 * F - 1) * ldw + K) * 2;
   if (ab >= (long)OOB || wb >= (long)OOB) return SDMOE_ESHAPE;
   p.a_bytes = (int)ab; p.w_bytes = (int)wb;
@@ -1695,6 +1718,6 @@ extern "C" int sdmoe_tune(int knob, int value) {
   if (knob == 6 && value >= 0 && value <= 63) { g_diag = value; return SDMOE_OK; }
   if (knob == 8 && (value == 0 || value == 1)) { g_res16 = value; return SDMOE_OK; }
   if (knob == 15 && (value == 0 || value == 1 || value == 4)) { g_topk_tpw = value; return SDMOE_OK; }
-  if (knob == 16 && (value == 0 || value == 1)) { g_halo = value; return SDMOE_OK; }
+  if (knob == 16 && value >= 0 && value <= 2) { g_halo = value; return SDMOE_OK; }
   return SDMOE_EARG;
 }

@@ -82,7 +82,10 @@ def load(path: str | None = None):
             "(or `make -C diffusion-models-moe_amd/csrc`). There is no CPU fallback."
         )
     lib = ctypes.CDLL(p)
+    ab_lib = "SDMOE_LIB" in os.environ  # same-box A/B against an older build: entry points it lacks stay unbound
     for name, argt in SIGNATURES.items():
+        if ab_lib and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.argtypes = argt
         fn.restype = ctypes.c_char_p if name == "sdmoe_version" else ctypes.c_int

@@ -495,8 +495,10 @@ def ensure_gelu_table(device) -> torch.Tensor:
     if t is None:
         vals = torch.nn.functional.gelu(gelu_table_values())  # fp16 CPU, as the reference's fp16 gate
         t = vals.to(torch.device("cuda", idx)).contiguous()
-        with torch.cuda.device(idx):
-            _lib.check(_lib.load().sdmoe_set_gelu_table(t.data_ptr()), "sdmoe_set_gelu_table")
+        lib = _lib.load()
+        if hasattr(lib, "sdmoe_set_gelu_table"):  # (an older A/B build evaluates GELU itself)
+            with torch.cuda.device(idx):
+                _lib.check(lib.sdmoe_set_gelu_table(t.data_ptr()), "sdmoe_set_gelu_table")
         _GELU_TABLES[idx] = t
     return t
 

@@ -418,7 +418,7 @@ def test_conv3x3_halo_tiles(H, Cin, Cout, nimg, up):
     wc = ops.conv_weight(w)
     outs = []
     kw = {} if up else dict(coladd=temb, coladd_bstride=Cout, residual=res)
-    for halo in (1, 0):
+    for halo in (2, 0):  # 2: every halo tile, including the 128-row ones the default leaves off
         _with_tune([(16, halo)], lambda: outs.append(ops.conv3x3(x, nimg, H, H, wc, b, upsample=up, **kw)))
     close(outs[0], ref)
     close(outs[1], ref)
