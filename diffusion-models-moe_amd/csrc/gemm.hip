@@ -94,6 +94,9 @@ struct GemmParams {
   const float* colf; long colf_bstride;
   // routed GEGLU with act == GELU: the registered fp16 GELU table (gelu_tab_h), staged into LDS for the epilogue
   const half_t* gelu_tab;
+  // halo conv: GroupNorm(+SiLU) of the main input applied to each staged halo slice (sdmoe_conv3x3_gn): per image
+  // and channel fp32 scale / shift ([nimg][Cin]); null = the input is used as is
+  const float* gn_scale; const float* gn_shift; int gn_silu;
 };
 
 SDMOE_DEV int swz(int row) { return (row >> 1) & 7; }
@@ -264,6 +267,8 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
   constexpr int A2BYTES = BM * RB;
   constexpr int HBYTES = H_INS * 1024 > 2 * A2BYTES ? H_INS * 1024 : 2 * A2BYTES, BSTAGE = BN * RB;
   constexpr int RING = HALO ? 2 * HBYTES + NSTAGE * BSTAGE : NSTAGE * STAGE;  // main-loop LDS
+  constexpr int GN_MAXC = 1280;                                   // halo conv GroupNorm: fp32 scale + shift per channel
+  constexpr int RINGX = RING + (HALO && !HUP ? GN_MAXC * 8 : 0);
   constexpr int RS16 = WN + 8;
   constexpr int NPASS16 = (NW * WM * RS16 * 2 <= RING) ? 1 : (NW * (WM / 2) * RS16 * 2 <= RING) ? 2
                           : ((NW * (WM / 4) * RS16 * 2 <= RING) ? 4 : 8);
@@ -272,7 +277,7 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
   static_assert(FM % NPASS == 0 && FM % NPASS16 == 0, "epilogue passes must split the wave's fragment rows");
   constexpr int EPI = NW * (WM / NPASS) * WN_PAD * 4;
   constexpr int EPI16 = NW * (WM / NPASS16) * RS16 * 2;
-  constexpr int SMEM0 = (RING > EPI) ? (RING > EPI16 ? RING : EPI16) : (EPI > EPI16 ? EPI : EPI16);
+  constexpr int SMEM0 = (RINGX > EPI) ? (RINGX > EPI16 ? RINGX : EPI16) : (EPI > EPI16 ? EPI : EPI16);
   constexpr int LUT_OFF = SMEM0;                 // MODE_KEEP: 16-entry nibble -> lane-mask table behind everything
   constexpr int SMEM1 = SMEM0 + (KEEP ? KEEP_LUT_BYTES : 0);
   // LN: per tile row (rstd, -mean*rstd), then the tile's BN columns of wsum and ln_bias (fp32), behind everything
@@ -595,10 +600,60 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
         a1 = n1;
       }
     };
+    // GroupNorm(+SiLU) of the main input (sdmoe_conv3x3_gn): this image's per-channel scale / shift go to LDS first;
+    // every staged halo slice is then normalised in place -- slice c + 1 at tap 5 of slice c (its pieces are older
+    // than that step's group, so landed; nobody reads its buffer before slice c + 1), the first one before its taps.
+    // Thread tid always holds 16-B chunk position tid % 4 of halo rows tid / 4 + 128 k, i.e. data chunk
+    // (tid % 4) ^ swzk(row) = (tid % 4) ^ ((tid >> 3) & 3): eight fixed channels. Out-of-image pixels stay zero (the
+    // conv pads the NORMALISED tensor). Same arithmetic as gn_apply_kernel: the conv input is bit-identical.
+    const bool gn = !HUP && p.gn_scale != nullptr;
+    float* const gsc = reinterpret_cast<float*>(smem + RING);
+    float* const gsh = gsc + GN_MAXC;
+    if constexpr (!HUP) {
+      if (gn) {
+        for (int i = tid; i < p.Cin; i += NT) {
+          gsc[i] = p.gn_scale[(long)bimg * p.Cin + i];
+          gsh[i] = p.gn_shift[(long)bimg * p.Cin + i];
+        }
+        __syncthreads();
+      }
+    }
+    auto transform = [&](int c32, int hb) {
+      if constexpr (!HUP) {
+        static_assert(NT == 512 && RB == 64, "transform mapping: 128 halo rows of 4 chunks per pass");
+        const int q = tid & 3, ch0 = c32 * 32 + ((q ^ ((tid >> 3) & 3)) << 3);
+        const float4v s0 = *reinterpret_cast<const float4v*>(gsc + ch0), s1 = *reinterpret_cast<const float4v*>(gsc + ch0 + 4);
+        const float4v h0 = *reinterpret_cast<const float4v*>(gsh + ch0), h1 = *reinterpret_cast<const float4v*>(gsh + ch0 + 4);
+        const float sc[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+        const float sh[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+        char* const buf = hbase + hb * HBYTES + q * 16;
+#pragma unroll
+        for (int k = 0; k < (HROWS_IN * HP + 127) / 128; ++k) {
+          const int row = (tid >> 2) + 128 * k;
+          const int r = row / HP, c = row - r * HP;
+          const int ih = oh0 - 1 + r, iw = c - 1;
+          if (row < HROWS_IN * HP && ih >= 0 && ih < p.H && iw >= 0 && iw < HW_) {
+            half8 v = *reinterpret_cast<const half8*>(buf + row * RB);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              float f = (float)v[j] * sc[j] + sh[j];
+              if (p.gn_silu) f = silu_f(f);
+              v[j] = (half_t)f;
+            }
+            *reinterpret_cast<half8*>(buf + row * RB) = v;
+          }
+        }
+      }
+    };
     if (nkl > 0) {
       if (nsl > 0) issue_halo(c_first, 0);
       issue_group(0);
       if (nkl > 1) issue_group(1);
+      if (gn && nsl > 0) {  // the first slice's halo (the oldest load) landed, visible to all, normalised
+        vm_wait(nkl > 1 ? group_cnt(0) + group_cnt(1) : group_cnt(0));
+        __syncthreads();
+        transform(c_first, 0);
+      }
     }
     for (int cs = 0; cs < nsl; ++cs) {
       const int hb = cs & 1;
@@ -616,6 +671,7 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
         asm volatile("" ::: "memory");
         if (ks + 2 < nkl && !(p.diag & 1)) issue_group(ks + 2);
         if (t == 0 && more && !(p.diag & 1)) issue_halo(c_first + cs + 1, hb ^ 1);
+        if (t == 5 && more && gn) transform(c_first + cs + 1, hb ^ 1);
         if (p.diag & 2) return;
         mfma_step(bbase + (t % 3) * BSTAGE + wc * WN * RB, [&](int i) -> half8 {
           const int i16 = 16 * i;
@@ -1669,6 +1725,33 @@ extern "C" int sdmoe_conv3x3_sc(const void* X, long ldx, int nimg, int H, int W,
   const int hs = try_halo(p, workspace, workspace_floats, (hipStream_t)stream);
   if (hs >= 0) return hs;
   return dispatch<MODE_CONV>(p, workspace, workspace_floats, (hipStream_t)stream);
+}
+
+extern "C" int sdmoe_conv3x3_gn(const void* X, long ldx, int nimg, int H, int W, int Cin, const float* gn_scale,
+                                const float* gn_shift, int silu, const void* Wt, const void* bias, const void* coladd,
+                                long coladd_bstride, const void* R, long ldr, const void* X2, long ldx2, int Cin2,
+                                void* Y, long ldy, int Cout, float* workspace, long workspace_floats, void* stream) {
+  if (nimg == 0) return SDMOE_OK;
+  if (!X || !gn_scale || !gn_shift || !Wt || !Y || nimg < 0 || H <= 0 || W <= 0 || Cout <= 0 || Cin2 < 0) return SDMOE_EARG;
+  if (Cin % 64 || Cin2 % 64 || Cout % 8 || ldx % 8 || ldy % 8 || (R && ldr % 8) || (X2 && ldx2 % 8)) return SDMOE_ESHAPE;
+  if ((X2 != nullptr) != (Cin2 > 0) || (X2 && R)) return SDMOE_EARG;
+  // only the halo tiles apply the GroupNorm in the kernel: the caller falls back to apply + conv on EUNSUP
+  if (!g_halo || g_tile || Cin > 1280 || Cout % 320 || W != 64 || (H * W) % 256) return SDMOE_EUNSUP;
+  GemmParams p{};
+  p.A = (const half_t*)X; p.lda = ldx; p.W = (const half_t*)Wt; p.ldw = 9L * Cin + Cin2;
+  p.bias = (const half_t*)bias; p.coladd = (const half_t*)coladd; p.coladd_bstride = coladd_bstride;
+  p.R = (const half_t*)R; p.ldr = ldr; p.C = (half_t*)Y; p.ldc = ldy;
+  p.M = nimg * H * W; p.N = Cout; p.K = 9 * Cin + Cin2; p.act = ACT_NONE;
+  p.rows_per_batch = H * W;
+  p.H = H; p.Wd = W; p.Cin = Cin; p.OH = H; p.OW = W; p.stride = 1; p.upsample = 0;
+  p.A2 = (const half_t*)X2; p.lda2 = ldx2;
+  p.gn_scale = gn_scale; p.gn_shift = gn_shift; p.gn_silu = silu;
+  const long ab = ((long)nimg * H * W - 1) * ldx * 2 + (long)Cin * 2, wb = (long)Cout * p.ldw * 2;
+  const long a2b = X2 ? ((long)nimg * H * W - 1) * ldx2 * 2 + (long)Cin2 * 2 : 0;
+  if (ab >= (long)OOB || wb >= (long)OOB || a2b >= (long)OOB) return SDMOE_ESHAPE;
+  p.a_bytes = (int)ab; p.w_bytes = (int)wb; p.a2_bytes = (int)a2b;
+  const int hs = try_halo(p, workspace, workspace_floats, (hipStream_t)stream);
+  return hs >= 0 ? hs : SDMOE_EUNSUP;
 }
 
 extern "C" int sdmoe_groupnorm_apply(const void* X, long ldx, int nimg, int HW, int C, const float* scale,

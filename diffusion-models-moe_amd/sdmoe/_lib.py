@@ -22,6 +22,8 @@ SIGNATURES = {
     "sdmoe_linear": [_P, _L, _P, _L, _P, _P, _L, _I, _P, _L, _P, _L, _I, _I, _I, _I, _P, _L, _P],
     "sdmoe_conv3x3": [_P, _L, _I, _I, _I, _I, _P, _P, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _P, _L, _P],
     "sdmoe_conv3x3_sc": [_P, _L, _I, _I, _I, _I, _P, _P, _P, _L, _P, _L, _I, _P, _L, _I, _I, _P, _L, _P],
+    "sdmoe_conv3x3_gn": [_P, _L, _I, _I, _I, _I, _P, _P, _I, _P, _P, _P, _L, _P, _L, _P, _L, _I, _P, _L, _I, _P, _L,
+                         _P],
     "sdmoe_groupnorm_apply": [_P, _L, _I, _I, _I, _P, _P, _I, _P, _L, _P],
     "sdmoe_mask_weight": [_P, _P, _L, _L, _P, _P],
     "sdmoe_groupnorm_stats": [_P, _L, _I, _I, _I, _I, _P, _P, _F, _P, _P, _P, _L, _P],

@@ -9,6 +9,8 @@ slices of a concatenation buffer, fused QKV outputs); spatial tensors are NHWC f
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib
@@ -215,6 +217,10 @@ def conv3x3(x, nimg, H, W, w, bias=None, *, stride=1, upsample=False, out=None, 
     w is then conv_weight_with_shortcut(...) [Cout, 9*Cin + Cin2]."""
     lib = _lib.load()
     if gn is not None:
+        if stride == 1 and not upsample and act == ACT_NONE and conv_gn_fusable(H, W, x.shape[1], w.shape[0]):
+            y = _conv3x3_gn(lib, x, nimg, H, W, w, bias, out, residual, coladd, coladd_bstride, gn, shortcut)
+            if y is not None:
+                return y
         x = groupnorm_apply(x, nimg, H * W, gn[0], gn[1], gn[2])
     xp, ldx = _rows(x, "x")
     Cin = x.shape[1]
@@ -249,6 +255,45 @@ def conv3x3(x, nimg, H, W, w, bias=None, *, stride=1, upsample=False, out=None, 
     rp, ldr = (None, 0) if residual is None else _rows(residual, "residual")
     return conv3x3_launch(xp, ldx, nimg, H, W, Cin, w, bias, coladd, coladd_bstride, rp, ldr, out, op, ldy, Cout,
                           stride, upsample, act)
+
+
+FUSED_GN = os.environ.get("SDMOE_FUSED_GN", "1") != "0"  # GroupNorm(+SiLU) inside the halo conv (0: apply pass)
+
+
+def conv_gn_fusable(H, W, Cin, Cout):
+    """Shapes whose conv applies a GroupNorm in the kernel (sdmoe_conv3x3_gn: the 64-wide halo tiles)."""
+    return FUSED_GN and W == 64 and (H * W) % 256 == 0 and Cin <= 1280 and Cin % 64 == 0 and Cout % 320 == 0
+
+
+def _conv3x3_gn(lib, x, nimg, H, W, w, bias, out, residual, coladd, coladd_bstride, gn, shortcut):
+    """conv3x3(act(GroupNorm(x))) with the norm applied to the staged input inside the conv; None if unsupported."""
+    xp, ldx = _rows(x, "x")
+    Cin, Cout = x.shape[1], w.shape[0]
+    if x.shape[0] != nimg * H * W:
+        raise ValueError("conv3x3: rows != nimg*H*W")
+    x2p, ldx2, Cin2 = None, 0, 0
+    if shortcut is not None:
+        x2p, ldx2 = _rows(shortcut, "shortcut")
+        Cin2 = shortcut.shape[1]
+        if w.dim() != 2 or w.shape[1] != 9 * Cin + Cin2 or residual is not None:
+            raise ValueError(f"conv3x3: weight {tuple(w.shape)} is not [Cout, 9*{Cin} + {Cin2}] or a residual was given")
+    elif w.dim() != 5 or tuple(w.shape[1:]) != (Cin // 64, 3, 3, 64):
+        raise ValueError(f"conv3x3: weight {tuple(w.shape)} is not the [Cout, Cin/64, 3, 3, 64] layout for Cin={Cin}")
+    sc, sh, silu = gn
+    if tuple(sc.shape) != (nimg, Cin) or sc.dtype != torch.float32 or tuple(sh.shape) != (nimg, Cin):
+        raise ValueError("conv3x3: gn scale / shift must be fp32 [nimg, Cin]")
+    if out is None:
+        out = torch.empty((nimg * H * W, Cout), dtype=torch.float16, device=x.device)
+    op, ldy = _rows(out, "out")
+    rp, ldr = (None, 0) if residual is None else _rows(residual, "residual")
+    ws = _workspace(out.device)
+    st = lib.sdmoe_conv3x3_gn(xp, ldx, nimg, H, W, Cin, sc.data_ptr(), sh.data_ptr(), int(bool(silu)), _dev(w, "w"),
+                              _ptr(bias), _ptr(coladd), coladd_bstride, rp, ldr, x2p, ldx2, Cin2, op, ldy, Cout,
+                              ws.data_ptr(), ws.numel(), _stream())
+    if st == -3:
+        return None
+    _lib.check(st, "sdmoe_conv3x3_gn")
+    return out
 
 
 def conv3x3_launch(xp, ldx, nimg, H, W, Cin, w, bias, coladd, coladd_bstride, rp, ldr, out, op, ldy, Cout, stride,

@@ -494,20 +494,32 @@ class ResnetBlock2D(nn.Module):
 
     def run(self, x, nimg, H, W, temb_all, out):
         HW = H * W
-        xn = self.norm1.normalize(x, nimg, HW, True)
         o, n = self.temb_slice
         # temb_all: [1, sum Cout] (SD-1.x, one timestep embedding for the batch) or [nimg, sum Cout] (SDXL:
         # per-image text_time conditioning) -> per-image column add in the conv epilogue
         bstride = temb_all.stride(0) if temb_all.shape[0] > 1 else 0
-        h = ops.conv3x3(xn, nimg, H, W, self.conv1.weight, self.conv1.bias,
-                        coladd=temb_all[:, o:o + n], coladd_bstride=bstride)
-        hn = self.norm2.normalize(h, nimg, HW, True)
+        cmid = self.conv1.weight.shape[0]
+        # GroupNorm + SiLU inside the conv where the halo tiles take it (sdmoe_conv3x3_gn: statistics only, no
+        # normalised copy of the activation written and re-read); elsewhere the one-call GroupNorm first
+        if ops.conv_gn_fusable(H, W, x.shape[1], cmid):
+            h = ops.conv3x3(x, nimg, H, W, self.conv1.weight, self.conv1.bias, coladd=temb_all[:, o:o + n],
+                            coladd_bstride=bstride, gn=self.norm1.stats(x, nimg, HW) + (True,))
+        else:
+            xn = self.norm1.normalize(x, nimg, HW, True)
+            h = ops.conv3x3(xn, nimg, H, W, self.conv1.weight, self.conv1.bias,
+                            coladd=temb_all[:, o:o + n], coladd_bstride=bstride)
+        gn2 = None
+        hn = h
+        if ops.conv_gn_fusable(H, W, cmid, self.conv2.weight.shape[0]):
+            gn2 = self.norm2.stats(h, nimg, HW) + (True,)
+        else:
+            hn = self.norm2.normalize(h, nimg, HW, True)
         if self.conv_shortcut is not None and FUSED_SC and x.shape[1] % 64 == 0:
             # conv2(hn) + conv_shortcut(x) in one implicit GEMM: the shortcut is K-steps over x at the output pixel
             w, b = self._conv2_with_shortcut()
-            return ops.conv3x3(hn, nimg, H, W, w, b, shortcut=x, out=out)
+            return ops.conv3x3(hn, nimg, H, W, w, b, shortcut=x, out=out, gn=gn2)
         res = x if self.conv_shortcut is None else self.conv_shortcut.run(x)
-        return ops.conv3x3(hn, nimg, H, W, self.conv2.weight, self.conv2.bias, residual=res, out=out)
+        return ops.conv3x3(hn, nimg, H, W, self.conv2.weight, self.conv2.bias, residual=res, out=out, gn=gn2)
 
 
 class Sampler(nn.Module):

@@ -71,6 +71,20 @@ int sdmoe_conv3x3_sc(const void* X, long ldx, int nimg, int H, int W, int Cin, c
 
 /* Y = (SiLU?)(X * scale[img, c] + shift[img, c]) on [nimg*HW, C] (the GroupNorm apply; scale/shift from
  * sdmoe_groupnorm_stats). C % 8 == 0. */
+/*
+ * Y = conv3x3(act(GroupNorm(X))) [+ X2 W_sc^T] (+ bias + coladd + R): the ResNet conv with the GroupNorm(+SiLU)
+ * in front of it applied INSIDE the conv (diffusers ResnetBlock2D: conv1(silu(norm1(x))), conv2(silu(norm2(h)))):
+ * gn_scale / gn_shift are the per-image, per-channel fp32 affine of sdmoe_groupnorm_stats ([nimg][Cin]); the
+ * normalised tensor is never written. Each 32-channel slice of the staged input halo is normalised once in LDS
+ * (zero padding stays zero), with sdmoe_groupnorm_apply's arithmetic, so Y equals sdmoe_groupnorm_apply followed by
+ * sdmoe_conv3x3 / sdmoe_conv3x3_sc bit for bit. X2 / Cin2: the optional folded 1x1 shortcut (raw input, not
+ * normalised; then R must be NULL). Only the halo-tiled shapes take it (W = 64, Cout % 320 == 0, Cin <= 1280):
+ * -3 (unsupported) otherwise -- the caller then applies the GroupNorm and calls sdmoe_conv3x3.
+ */
+int sdmoe_conv3x3_gn(const void* X, long ldx, int nimg, int H, int W, int Cin, const float* gn_scale,
+                     const float* gn_shift, int silu, const void* Wt, const void* bias, const void* coladd,
+                     long coladd_bstride, const void* R, long ldr, const void* X2, long ldx2, int Cin2, void* Y,
+                     long ldy, int Cout, float* workspace, long workspace_floats, void* stream);
 int sdmoe_groupnorm_apply(const void* X, long ldx, int nimg, int HW, int C, const float* scale, const float* shift,
                           int silu, void* Y, long ldy, void* stream);
 

@@ -425,6 +425,43 @@ def test_conv3x3_halo_tiles(H, Cin, Cout, nimg, up):
     close(outs[0], outs[1].float())
 
 
+@pytest.mark.parametrize("Cin,Cout,Cin2,nimg,res", [(320, 320, 0, 16, True), (960, 320, 0, 2, False), (640, 320, 0, 3, False),
+                                                   (320, 320, 640, 2, False), (320, 320, 960, 16, False)])
+def test_conv3x3_groupnorm_in_kernel_bit_identical(Cin, Cout, Cin2, nimg, res):
+    """sdmoe_conv3x3_gn (GroupNorm + SiLU applied to each staged halo slice inside the conv: 64-wide tiles) vs
+    sdmoe_groupnorm_apply + sdmoe_conv3x3(_sc): bit-identical output (same normalisation arithmetic, same conv K
+    order), incl. the folded shortcut, the residual / time-embedding epilogue, a concat-buffer input (row stride >
+    Cin) and K split over slices (nimg 2-3); vs torch fp32 within the kernel tolerance."""
+    H = 64
+    buf = rnd(nimg * H * H, Cin + 64, seed=Cin + Cin2) * 2 + 0.5
+    x = buf[:, 64:]
+    gamma, beta = rnd(Cin, scale=0.1, seed=1) + 1, rnd(Cin, scale=0.1, seed=2)
+    sc, sh = ops.groupnorm_stats(x, nimg, H * H, gamma, beta, 1e-5, 32)
+    w, b = rnd(Cout, 3, 3, Cin, scale=(9 * Cin) ** -0.5, seed=3), rnd(Cout, scale=0.1, seed=4)
+    temb = rnd(1, Cout, seed=5)
+    r = rnd(nimg * H * H, Cout, seed=6) if res else None
+    x2 = rnd(nimg * H * H, Cin2, seed=7) if Cin2 else None
+    if Cin2:
+        w2 = rnd(Cout, Cin2, scale=Cin2 ** -0.5, seed=8)
+        wc = ops.conv_weight_with_shortcut(ops.conv_weight(w), w2)
+        kw = dict(shortcut=x2)
+    else:
+        wc = ops.conv_weight(w)
+        kw = dict(coladd=temb, coladd_bstride=0, residual=r)
+    assert ops.conv_gn_fusable(H, H, Cin, Cout)
+    fused = ops.conv3x3(x, nimg, H, H, wc, b, gn=(sc, sh, True), **kw)
+    xn = ops.groupnorm_apply(x, nimg, H * H, sc, sh, True)
+    plain = ops.conv3x3(xn, nimg, H, H, wc, b, **kw)
+    assert torch.equal(fused, plain)
+    xr = F.silu(F.group_norm(x.float().view(nimg, H * H, Cin).permute(0, 2, 1), 32, gamma.float(), beta.float(), 1e-5))
+    ref = conv_ref(xr.permute(0, 2, 1).reshape(-1, Cin), nimg, H, H, w, b)
+    if Cin2:
+        ref = ref + x2.float() @ w2.float().t()
+    else:
+        ref = ref + temb.float() + (r.float() if res else 0)
+    close(fused, ref)
+
+
 def test_conv3x3_full_size_upsample_concat():
     """The 32x32 -> 64x64 upsample conv (640 ch) and a 64x64 skip-concat conv input (960 -> 320) at batch 16."""
     nimg = 16
