@@ -230,8 +230,11 @@ class KernelTimer:
                 timer.on_eval = False
         unet.forward_nhwc = wrapped
 
-    def wrap(self, ops_mod):
-        orig = getattr(ops_mod, self.family)
+    def wrap(self, ops_mod, family=None):
+        """Time every launch of `family` (default self.family); several families (the conv with and without the
+        in-kernel GroupNorm) can feed one timer."""
+        family = family or self.family
+        orig = getattr(ops_mod, family)
         timer = self
 
         def wrapped(*a, **k):
@@ -241,13 +244,14 @@ class KernelTimer:
             s.record()
             out = orig(*a, **k)
             e.record()
-            timer.pairs.append((s, e))
-            timer.account(a, k, out)
+            if out is not None:  # (sdmoe_conv3x3_gn declined the shape: nothing launched)
+                timer.pairs.append((s, e))
+                timer.account(a, k, out)
             return out
-        setattr(ops_mod, self.family, wrapped)
+        setattr(ops_mod, family, wrapped)
         import sdmoe.unet as U
-        if hasattr(U.ops, self.family):
-            setattr(U.ops, self.family, wrapped)
+        if hasattr(U.ops, family):
+            setattr(U.ops, family, wrapped)
 
     def account(self, a, k, out):
         # conv3x3_launch(xp, ldx, nimg, H, W, Cin, w, ...): algorithmic FLOPs = 2 * M * Cout * 9 * Cin (real
@@ -374,6 +378,7 @@ def main():
     timer = KernelTimer("conv3x3_launch", args.roofline_sample)
     if not args.no_roofline:
         timer.wrap(ops)
+        timer.wrap(ops, "conv3x3_gn_launch")  # the 64x64-level ResNet convs with their GroupNorm applied in-kernel
         timer.wrap_evals(pipe.unet)
     pipe.unet.conv_in.weight._sdmoe_conv_in = True
     pipe.unet.conv_out.weight._sdmoe_conv_out = True
@@ -446,8 +451,8 @@ def main():
                 # this bench command on the build named in the file
                 traffic_src = (f"{os.path.relpath(args.traffic, ROOT)} (rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes"
                                f" of bench.py, build {pmc.get('build', '?')})")
-            roof = {"bound": "mfma", "kernel": "sdmoe_conv3x3: implicit-GEMM conv (gemm_kernel<BM,BN,MODE=1|2,STAGES>"
-                                               " + split-K reduce where used)",
+            roof = {"bound": "mfma", "kernel": "sdmoe_conv3x3 / _sc / _gn: implicit-GEMM conv (gemm_kernel MODE 1/2 "
+                                               "shifted tiles, MODE 9/12 halo tiles, + split-K reduce where used)",
                     "achieved": round(achieved, 1), "peak": PEAK_FP16_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(achieved / PEAK_FP16_TFLOPS, 4), "traffic": traffic, "traffic_source": traffic_src,
                     "launches": n, "avg_launch_ms": round(ms / n, 4),

@@ -286,10 +286,20 @@ def _conv3x3_gn(lib, x, nimg, H, W, w, bias, out, residual, coladd, coladd_bstri
         out = torch.empty((nimg * H * W, Cout), dtype=torch.float16, device=x.device)
     op, ldy = _rows(out, "out")
     rp, ldr = (None, 0) if residual is None else _rows(residual, "residual")
+    return conv3x3_gn_launch(xp, ldx, nimg, H, W, Cin, w, bias, coladd, coladd_bstride, rp, ldr, out, op, ldy, Cout,
+                             (sc, sh, silu), sc=(x2p, ldx2, Cin2) if shortcut is not None else None)
+
+
+def conv3x3_gn_launch(xp, ldx, nimg, H, W, Cin, w, bias, coladd, coladd_bstride, rp, ldr, out, op, ldy, Cout, gn,
+                      sc=None):
+    """The sdmoe_conv3x3_gn launch alone (argument order of conv3x3_launch: bench.py times both families); None when
+    the shape is not one the kernel normalises itself."""
+    lib = _lib.load()
     ws = _workspace(out.device)
-    st = lib.sdmoe_conv3x3_gn(xp, ldx, nimg, H, W, Cin, sc.data_ptr(), sh.data_ptr(), int(bool(silu)), _dev(w, "w"),
-                              _ptr(bias), _ptr(coladd), coladd_bstride, rp, ldr, x2p, ldx2, Cin2, op, ldy, Cout,
-                              ws.data_ptr(), ws.numel(), _stream())
+    x2p, ldx2, Cin2 = sc if sc is not None else (None, 0, 0)
+    st = lib.sdmoe_conv3x3_gn(xp, ldx, nimg, H, W, Cin, gn[0].data_ptr(), gn[1].data_ptr(), int(bool(gn[2])),
+                              _dev(w, "w"), _ptr(bias), _ptr(coladd), coladd_bstride, rp, ldr, x2p, ldx2, Cin2, op, ldy,
+                              Cout, ws.data_ptr(), ws.numel(), _stream())
     if st == -3:
         return None
     _lib.check(st, "sdmoe_conv3x3_gn")
