@@ -1214,9 +1214,10 @@ int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s, int ks_w
   return SDMOE_OK;
 }
 
-// knob 16: halo-tiled stride-1 3x3 convs: 1 (default) = on the 256-row tiles (64-wide outputs: the 64x64 level and the
-// 32 -> 64 upsample conv) where they measured faster; 2 = also the 128-row tiles (32- / 16-wide outputs: 9-12 %
-// slower than the shifted-tile path there, their 32-deep K-steps carry half the MFMAs per barrier); 0 = off
+// knob 16: halo-tiled stride-1 3x3 convs: 1 (default) = where they measured faster than the shifted-tile kernel:
+// 64-wide outputs (256-row tiles), 16-wide ones on 256-row tiles (a whole image), the 32 -> 64 and 8 -> 16 upsample
+// convs; 2 = every 128-row tile instead (32- / 16-wide outputs: 5-17 % slower, their 32-deep K-steps carry half the
+// MFMAs per barrier); 0 = off
 int g_halo = 1;
 
 // halo conv launch: BM x 320 tiles (8 waves 2 x 4, BK 32, 3-stage B ring), K split over whole 32-channel slices when
@@ -1264,13 +1265,15 @@ int try_halo(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
     if (p.A2) return -1;
     const int ohw = 4 * p.H * p.Wd;
     if (p.Wd == 32 && ohw % 256 == 0) return launch_halo<256, MODE_CONVHUP64>(p, ws, ws_floats, s);
+    if (p.Wd == 8 && ohw % 128 == 0) return launch_halo<128, MODE_CONVHUP16>(p, ws, ws_floats, s);  // 125.6 vs 137.0
     if (g_halo < 2) return -1;
-    if (p.Wd == 16 && ohw % 128 == 0) return launch_halo<128, MODE_CONVHUP32>(p, ws, ws_floats, s);
-    if (p.Wd == 8 && ohw % 128 == 0) return launch_halo<128, MODE_CONVHUP16>(p, ws, ws_floats, s);
+    if (p.Wd == 16 && ohw % 128 == 0) return launch_halo<128, MODE_CONVHUP32>(p, ws, ws_floats, s);  // 449 vs 383 us
     return -1;
   }
   const int hw = p.H * p.Wd;
   if (p.Wd == 64 && hw % 256 == 0) return launch_halo<256, MODE_CONVH64>(p, ws, ws_floats, s);
+  // 16-wide outputs: a whole 16x16 image per 256-row tile, K split over slices (1280 -> 1280: 127.6 vs 133.0 us)
+  if (g_halo != 2 && p.Wd == 16 && hw % 256 == 0) return launch_halo<256, MODE_CONVH16>(p, ws, ws_floats, s);
   if (g_halo < 2) return -1;
   if (p.Wd == 32 && hw % 128 == 0) return launch_halo<128, MODE_CONVH32>(p, ws, ws_floats, s);
   if (p.Wd == 16 && hw % 128 == 0) return launch_halo<128, MODE_CONVH16>(p, ws, ws_floats, s);
@@ -1801,6 +1804,6 @@ extern "C" int sdmoe_tune(int knob, int value) {
   if (knob == 6 && value >= 0 && value <= 63) { g_diag = value; return SDMOE_OK; }
   if (knob == 8 && (value == 0 || value == 1)) { g_res16 = value; return SDMOE_OK; }
   if (knob == 15 && (value == 0 || value == 1 || value == 4)) { g_topk_tpw = value; return SDMOE_OK; }
-  if (knob == 16 && value >= 0 && value <= 2) { g_halo = value; return SDMOE_OK; }
+  if (knob == 16 && value >= 0 && value <= 3) { g_halo = value; return SDMOE_OK; }
   return SDMOE_EARG;
 }
