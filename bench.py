@@ -452,7 +452,7 @@ def main():
                 traffic_src = (f"{os.path.relpath(args.traffic, ROOT)} (rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes"
                                f" of bench.py, build {pmc.get('build', '?')})")
             roof = {"bound": "mfma", "kernel": "sdmoe_conv3x3 / _sc / _gn: implicit-GEMM conv (gemm_kernel MODE 1/2 "
-                                               "shifted tiles, MODE 9/12 halo tiles, + split-K reduce where used)",
+                                               "shifted tiles, MODE 9/11/12/14 halo tiles, + split-K reduce where used)",
                     "achieved": round(achieved, 1), "peak": PEAK_FP16_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(achieved / PEAK_FP16_TFLOPS, 4), "traffic": traffic, "traffic_source": traffic_src,
                     "launches": n, "avg_launch_ms": round(ms / n, 4),
