@@ -1215,9 +1215,10 @@ int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s, int ks_w
 }
 
 // knob 16: halo-tiled stride-1 3x3 convs: 1 (default) = where they measured faster than the shifted-tile kernel:
-// 64-wide outputs (256-row tiles), 16-wide ones on 256-row tiles (a whole image), the 32 -> 64 and 8 -> 16 upsample
-// convs; 2 = every 128-row tile instead (32- / 16-wide outputs: 5-17 % slower, their 32-deep K-steps carry half the
-// MFMAs per barrier); 0 = off
+// 64-wide outputs (256-row tiles), 16-wide ones on 256-row tiles (a whole image), the 32 -> 64, 16 -> 32 (256-row
+// tiles) and 8 -> 16 upsample convs; 2 = every 128-row tile instead (32- / 16-wide outputs: 5-17 % slower, their
+// 32-deep K-steps carry half the MFMAs per barrier); 3 = the default plus 32-wide outputs on 256-row tiles (135.1 vs
+// 118.0 us at 640 -> 640: not kept); 0 = off
 int g_halo = 1;
 
 // halo conv launch: BM x 320 tiles (8 waves 2 x 4, BK 32, 3-stage B ring), K split over whole 32-channel slices when
@@ -1266,6 +1267,8 @@ int try_halo(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
     const int ohw = 4 * p.H * p.Wd;
     if (p.Wd == 32 && ohw % 256 == 0) return launch_halo<256, MODE_CONVHUP64>(p, ws, ws_floats, s);
     if (p.Wd == 8 && ohw % 128 == 0) return launch_halo<128, MODE_CONVHUP16>(p, ws, ws_floats, s);  // 125.6 vs 137.0
+    // 16 -> 32 upsample on 256-row tiles (8 output rows, K split over slices): 360.3 vs 383.1-395.8 us
+    if (g_halo != 2 && p.Wd == 16 && ohw % 256 == 0) return launch_halo<256, MODE_CONVHUP32>(p, ws, ws_floats, s);
     if (g_halo < 2) return -1;
     if (p.Wd == 16 && ohw % 128 == 0) return launch_halo<128, MODE_CONVHUP32>(p, ws, ws_floats, s);  // 449 vs 383 us
     return -1;
@@ -1274,6 +1277,7 @@ int try_halo(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
   if (p.Wd == 64 && hw % 256 == 0) return launch_halo<256, MODE_CONVH64>(p, ws, ws_floats, s);
   // 16-wide outputs: a whole 16x16 image per 256-row tile, K split over slices (1280 -> 1280: 127.6 vs 133.0 us)
   if (g_halo != 2 && p.Wd == 16 && hw % 256 == 0) return launch_halo<256, MODE_CONVH16>(p, ws, ws_floats, s);
+  if (g_halo == 3 && p.Wd == 32 && hw % 256 == 0) return launch_halo<256, MODE_CONVH32>(p, ws, ws_floats, s);
   if (g_halo < 2) return -1;
   if (p.Wd == 32 && hw % 128 == 0) return launch_halo<128, MODE_CONVH32>(p, ws, ws_floats, s);
   if (p.Wd == 16 && hw % 128 == 0) return launch_halo<128, MODE_CONVH16>(p, ws, ws_floats, s);

@@ -289,9 +289,128 @@ __global__ __launch_bounds__(64 * 16 / TPW) void moe_topk_mask_kernel(
   }
 }
 
+// DPP moves inside a quad of lanes (quad_perm): lane q reads lane SEL(q)
+template <int CTRL>
+SDMOE_DEV uint32_t quad_mov(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
+}
+constexpr int QP_XOR1 = 0xB1, QP_XOR2 = 0x4E, QP_B0 = 0x00, QP_B1 = 0x55, QP_B2 = 0xAA, QP_B3 = 0xFF;
+
+// Top-k keep bits for E <= 64 experts with ONE QUAD OF LANES PER TOKEN (16 tokens per wave): lane q of a quad holds
+// the order keys of experts 16 q .. 16 q + 15 in registers and runs the same 16-bit radix search as above on them,
+// its counts summed over the quad with two DPP adds per bit -- no ballots, no SALU chain, 4096 independent waves at
+// M = 65536 (the ballot kernel's serial per-token chain left it at ~28 us there). Same selection rule: the k
+// largest keys, ties at the k-th key toward the lowest expert id. Each lane then writes every 4th 64-neuron keep
+// word of its token (16 tokens x 8 B per word and quad lane: whole 128-B lines).
+// FULL (E = 64 experts of 20 neurons, 16-B aligned score rows -- every 64x64-level FFN of SD-1.4): no validity
+// masks, and lane q's 16 experts are exactly neurons 320 q .. 320 q + 319, i.e. keep words 5 q .. 5 q + 4, whose
+// expert -> bit-range pattern is then a compile-time constant (only the lane's own keep bits enter them).
+template <bool FULL, int SC>  // compile-time expert size (0 = runtime S)
+__global__ __launch_bounds__(256) void moe_topk_keep_quad_kernel(
+    int M, int F, int E, int S_, int k, const half_t* __restrict__ score, long lds,
+    const uint32_t* __restrict__ removed, uint32_t* __restrict__ sel_out, unsigned long long* __restrict__ keep) {
+  static_assert(!FULL || SC == 20, "FULL: 64 experts of 20 neurons");
+  const int S = SC ? SC : S_;
+  const int lane = threadIdx.x & 63, q = lane & 3;
+  const int m = blockIdx.x * 64 + (threadIdx.x >> 2);
+  const int mc = min(m, M - 1);
+  const half_t* srow = score + (long)mc * lds + 16 * q;
+  half_t s[16];
+  if constexpr (FULL) {  // E == 64, 16-B aligned rows
+    const half8 a = *reinterpret_cast<const half8*>(srow), b = *reinterpret_cast<const half8*>(srow + 8);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { s[i] = a[i]; s[8 + i] = b[i]; }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s[i] = srow[min(16 * q + i, E - 1) - 16 * q];
+  }
+  const uint64_t rm64 = removed ? ((uint64_t)removed[0] | (E > 32 ? (uint64_t)removed[1] << 32 : 0ull)) : 0ull;
+  const uint32_t rm16 = (uint32_t)(rm64 >> (16 * q)) & 0xffffu;
+  const int nval = min(max(E - 16 * q, 0), 16);  // valid experts of this lane
+  const uint32_t vmask = FULL || nval >= 16 ? 0xffffu : ((1u << nval) - 1u);
+  uint32_t key[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) key[i] = order_key(((rm16 >> i) & 1u) ? (half_t)0.f : s[i]);
+  auto quad_sum = [](uint32_t c) {
+    c += quad_mov<QP_XOR1>(c);
+    return c + quad_mov<QP_XOR2>(c);
+  };
+  uint32_t T = 0;
+  for (int bit = 15; bit >= 0; --bit) {
+    const uint32_t cand = T | (1u << bit);
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) c += (((vmask >> i) & 1u) && key[i] >= cand) ? 1u : 0u;
+    if ((int)quad_sum(c) >= k) T = cand;
+  }
+  uint32_t gt = 0, ties = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const bool v = (vmask >> i) & 1u;
+    gt += (v && key[i] > T) ? 1u : 0u;
+    ties += (v && key[i] == T) ? 1u : 0u;
+  }
+  const int need = k - (int)quad_sum(gt);
+  // ties of the quad's lower lanes (lower expert ids) come first
+  const uint32_t t0 = quad_mov<QP_B0>(ties), t1 = quad_mov<QP_B1>(ties), t2 = quad_mov<QP_B2>(ties);
+  int r = (q > 0 ? (int)t0 : 0) + (q > 1 ? (int)t1 : 0) + (q > 2 ? (int)t2 : 0);
+  uint32_t sel16 = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const bool v = (vmask >> i) & 1u;
+    const bool tie = v && key[i] == T;
+    const bool sel = k > 0 && v && (key[i] > T || (tie && r < need));
+    r += tie ? 1 : 0;
+    sel16 |= (sel ? 1u : 0u) << i;
+  }
+  const uint32_t keep16 = sel16 & ~rm16;
+  // the token's 64 selection / keep bits in every lane of the quad
+  const uint32_t slo = quad_mov<QP_B0>(sel16) | (quad_mov<QP_B1>(sel16) << 16);
+  const uint32_t shi = quad_mov<QP_B2>(sel16) | (quad_mov<QP_B3>(sel16) << 16);
+  const uint64_t keep64 = (uint64_t)(quad_mov<QP_B0>(keep16) | (quad_mov<QP_B1>(keep16) << 16)) |
+                          ((uint64_t)(quad_mov<QP_B2>(keep16) | (quad_mov<QP_B3>(keep16) << 16)) << 32);
+  if (m >= M) return;
+  if (sel_out && q < ((E + 31) >> 5)) sel_out[(long)m * ((E + 31) >> 5) + q] = q ? shi : slo;
+  if constexpr (FULL) {
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      unsigned long long w = 0;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int lo = max(20 * i, 64 * j) - 64 * j, hi = min(20 * i + 20, 64 * j + 64) - 64 * j;
+        if (hi > lo) w |= ((keep16 >> i) & 1u) ? ((1ull << (hi - lo)) - 1ull) << lo : 0ull;
+      }
+      keep[(long)(5 * q + j) * M + m] = w;
+    }
+    (void)keep64;
+    return;
+  }
+  const int nks = F >> 6;
+  for (int ks = q; ks < nks; ks += 4) {
+    const int n0 = 64 * ks, e0 = n0 / S, e1 = min((n0 + 63) / S, E - 1);
+    unsigned long long w = 0;
+    auto add = [&](int e) {
+      if ((keep64 >> e) & 1ull) {
+        const int lo = max(e * S, n0) - n0, hi = min((e + 1) * S, n0 + 64) - n0;
+        w |= (hi - lo >= 64 ? ~0ull : ((1ull << (hi - lo)) - 1ull)) << lo;
+      }
+    };
+    if constexpr (SC > 0) {
+      constexpr int SPAN = 64 / (SC > 0 ? SC : 1) + 2;  // experts one 64-neuron word can overlap
+#pragma unroll
+      for (int d = 0; d < SPAN; ++d)
+        if (e0 + d <= e1) add(e0 + d);
+    } else {
+      for (int e = e0; e <= e1; ++e) add(e);
+    }
+    keep[(long)ks * M + m] = w;
+  }
+}
+
 }  // namespace
 
-int g_topk_tpw = 0;  // sdmoe_tune knob 15: 0 = by M (default), 1 / 4 = always 1 / 4 tokens per wave
+int g_topk_tpw = 0;  // sdmoe_tune knob 15: 0 = by M (default; keep bits at E <= 64: one quad per token), 1 / 4 =
+                     // always the ballot kernel at 1 / 4 tokens per wave
 
 template <bool KEEPOUT>
 int launch_topk(half_t* P, long ldp, int M, int F, int E, int esize, int k, const half_t* sc, long ld_score,
@@ -338,6 +457,22 @@ extern "C" int sdmoe_moe_topk_keep(int M, int F, int E, int esize, int k, const 
   if (F % 64 || E * esize != F || ld_score < E) return SDMOE_ESHAPE;
   if (E > 256 || esize > 40) return SDMOE_EUNSUP;
   if (k < 0 || k > E) return SDMOE_EARG;
+  if (E <= 64 && g_topk_tpw == 0) {
+    const bool full = E == 64 && esize == 20 && ld_score % 8 == 0 && ((uintptr_t)score & 15) == 0;
+    hipStream_t s = (hipStream_t)stream;
+    const int g = (M + 63) / 64;
+    const half_t* sc = (const half_t*)score;
+    const uint32_t* rm = (const uint32_t*)removed_bits;
+    unsigned long long* kp = (unsigned long long*)keep;
+    if (full)
+      moe_topk_keep_quad_kernel<true, 20><<<g, 256, 0, s>>>(M, F, E, esize, k, sc, ld_score, rm, sel_out, kp);
+    else if (esize == 20)
+      moe_topk_keep_quad_kernel<false, 20><<<g, 256, 0, s>>>(M, F, E, esize, k, sc, ld_score, rm, sel_out, kp);
+    else
+      moe_topk_keep_quad_kernel<false, 0><<<g, 256, 0, s>>>(M, F, E, esize, k, sc, ld_score, rm, sel_out, kp);
+    SDMOE_CHECK_LAUNCH();
+    return SDMOE_OK;
+  }
   return launch_topk<true>(nullptr, 0, M, F, E, esize, k, (const half_t*)score, ld_score, (const uint32_t*)removed_bits,
                            sel_out, (unsigned long long*)keep, (hipStream_t)stream);
 }

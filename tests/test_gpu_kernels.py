@@ -404,8 +404,8 @@ def test_conv3x3_full_size_tiles(tile, stages):
                                                 (32, 640, 640, 2, True), (16, 1280, 1280, 16, True),
                                                 (8, 1280, 1280, 3, True)])
 def test_conv3x3_halo_tiles(H, Cin, Cout, nimg, up):
-    """Halo-tiled stride-1 convs (MODE_CONVH64/32/16 and the 2x-upsample MODE_CONVHUP64/32/16, sdmoe_tune knob 16 = 1,
-    default): the input halo of each 32-channel slice staged once for the 9 taps, incl. image borders, K split over
+    """Halo-tiled stride-1 convs (MODE_CONVH64/32/16 and the 2x-upsample MODE_CONVHUP64/32/16, every sdmoe_tune knob 16
+    setting): the input halo of each 32-channel slice staged once for the 9 taps, incl. image borders, K split over
     slices (small grids: nimg 2-4) and the time-embedding column add + residual epilogue; vs torch fp32 and vs the
     shifted-tile path (knob 16 = 0) within the same tolerance (the K order differs: 32- vs 64-channel slices)."""
     OH = 2 * H if up else H
@@ -418,11 +418,13 @@ def test_conv3x3_halo_tiles(H, Cin, Cout, nimg, up):
     wc = ops.conv_weight(w)
     outs = []
     kw = {} if up else dict(coladd=temb, coladd_bstride=Cout, residual=res)
-    for halo in (2, 0):  # 2: every halo tile, including the 128-row ones the default leaves off
+    # 1 default; 2: the 128-row halo tiles the default leaves off; 3: 32-wide outputs on 256-row tiles; 0: shifted
+    for halo in (1, 2, 3, 0):
         _with_tune([(16, halo)], lambda: outs.append(ops.conv3x3(x, nimg, H, H, wc, b, upsample=up, **kw)))
-    close(outs[0], ref)
-    close(outs[1], ref)
-    close(outs[0], outs[1].float())
+    for o in outs:
+        close(o, ref)
+    for o in outs[:3]:
+        close(o, outs[3].float())
 
 
 @pytest.mark.parametrize("Cin,Cout,Cin2,nimg,res", [(320, 320, 0, 16, True), (960, 320, 0, 2, False), (640, 320, 0, 3, False),

@@ -304,6 +304,52 @@ def test_topk_one_token_per_wave_matches_four(M, E, k, nrem):
     assert torch.equal(res[0][1], res[0][2])
 
 
+@pytest.mark.parametrize("M,E,k,nrem,esize,ld", [(65536, 64, 12, 5, 20, 64), (4097, 64, 13, 0, 20, 64),
+                                                  (1000, 64, 64, 3, 20, 72), (333, 48, 9, 2, 20, 48),
+                                                  (70, 32, 6, 1, 20, 33), (129, 64, 0, 0, 20, 64),
+                                                  (500, 64, 12, 4, 10, 64), (256, 16, 4, 0, 40, 16)])
+def test_topk_keep_quad_kernel(M, E, k, nrem, esize, ld):
+    """sdmoe_moe_topk_keep at E <= 64 (one quad of lanes per token, the default there) vs the ballot kernel (sdmoe_tune
+    knob 15 = 4) and vs a numpy restatement of the selection rule (moefy.py:20-23 top-k; ties at the k-th score
+    toward the lowest expert id; removed experts score 0 and are never kept): identical keep words and selection bits,
+    on scores quantised to force ties, with M tails, strided / unaligned score rows (ld != E), k = 0 and k = E."""
+    from sdmoe import _lib
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(M + 7 * E + k)
+    F = E * esize
+    routing = ops.Routing(torch.arange(F) // esize, E, k, DEV)
+    full = (torch.randint(-3, 12, (M, ld), generator=g).float() / 4).half()
+    score = full.to(DEV)[:, :E]
+    rm_list = torch.randperm(E, generator=g)[:nrem].tolist()
+    removed = ops.removed_bits(rm_list, E, DEV) if nrem else None
+    res = {}
+    for tpw in (0, 4):
+        _lib.check(lib.sdmoe_tune(15, tpw), "tune")
+        try:
+            sel = torch.zeros((M, (E + 31) // 32), dtype=torch.int32, device=DEV)
+            keep = ops.moe_topk_keep(score, routing, M, removed=removed, sel_out=sel)
+            torch.cuda.synchronize()
+            res[tpw] = (sel.cpu(), keep.cpu())
+        finally:
+            _lib.check(lib.sdmoe_tune(15, 0), "tune")
+    assert torch.equal(res[0][0], res[4][0])
+    assert torch.equal(res[0][1], res[4][1])
+    # numpy: stable descending order of the fp16 scores (removed -> 0; -0 == +0), first k are selected
+    s = full[:, :E].float().numpy().copy()
+    s[:, rm_list] = 0.0
+    order = np.argsort(-s, axis=1, kind="stable")[:, :k]
+    selb = np.zeros((M, E), bool)
+    np.put_along_axis(selb, order, True, axis=1)
+    got = sel_bits_to_bool(res[0][0], E)
+    assert np.array_equal(got, selb)
+    keepb = selb.copy()
+    keepb[:, rm_list] = False
+    neur = np.repeat(keepb, esize, axis=1)  # [M, F]
+    kb = res[0][1].numpy().view(np.uint64)  # [F/64, M]
+    bits = ((kb[:, :, None] >> np.arange(64, dtype=np.uint64)) & np.uint64(1)).astype(bool)
+    assert np.array_equal(bits.transpose(1, 0, 2).reshape(M, F), neur)
+
+
 @pytest.mark.parametrize("M", [64, 4096, 8192])  # 64x160 (table loaded after the K loop), 128x160, 256x320 tiles
 def test_gelu_every_fp16_input_matches_reference_activation(M):
     """The GEGLU kernels' GELU on EVERY finite fp16 gate value vs the reference's activation itself (F.gelu on an fp16

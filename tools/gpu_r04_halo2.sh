@@ -1,8 +1,8 @@
 #!/bin/bash
-# conv rows under the halo knob settings (16 = 0 off, 1 default, 2 all 128-row tiles, 3 16-wide on 256-row tiles)
+# conv rows under the halo knob settings (16 = 0 off, 1 default, 2 all 128-row tiles, 3 32-wide on 256-row tiles too)
 set -u
 mkdir -p gpurun_out/r04h2
-for h in 1 2 3 0; do
+for h in ${HALO_KNOBS:-1 3 0}; do
   echo "== halo knob $h"
   SDMOE_TUNE="16=$h" timeout -k 10 300 python tools/gemm_bench.py --only conv --iters 10 > gpurun_out/r04h2/conv_h$h.log 2>&1 || { echo "FAILED"; tail -5 gpurun_out/r04h2/conv_h$h.log; exit 1; }
   grep conv gpurun_out/r04h2/conv_h$h.log

@@ -5,7 +5,10 @@ usage: python tools/pmc_traffic.py FETCH_counter_collection.csv WRITE_counter_co
 
 gfx950 corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE (KiB) reports exactly half of the bytes of wide
 coalesced streaming reads (16 B/lane loads and LDS-DMA alike) -> doubled; WRITE_SIZE (KiB) is exact for
-16-B-per-lane stores. Counters are collected in separate passes (one counter group per run)."""
+16-B-per-lane stores. Counters are collected in separate passes (one counter group per run).
+
+A split-K launch is two dispatches (the fp32 partial slabs, then splitk_reduce_kernel): a reduce dispatch that directly
+follows a kept gemm dispatch is charged to that launch, so bytes_per_launch is per conv op, as bench.py times it."""
 import argparse
 import csv
 import json
@@ -31,8 +34,9 @@ def main():
     ap.add_argument("fetch_csv")
     ap.add_argument("write_csv")
     ap.add_argument("--kernel", default="gemm_kernel<")
-    ap.add_argument("--mode", default="1,2", help="comma list of gemm_kernel MODE values (5th template arg: "
-                    "1 = conv, 2 = conv with fused upsample); '' = any")
+    ap.add_argument("--mode", default="1,2,9,10,11,12,13,14",
+                    help="comma list of gemm_kernel MODE values (5th template arg: 1 = conv, 2 = conv with fused "
+                    "upsample, 9-11 halo conv, 12-14 halo conv with fused upsample); '' = any")
     ap.add_argument("--out", default=None)
     ap.add_argument("--build", default="", help="git revision of the measured build (recorded in the json)")
     a = ap.parse_args()
@@ -48,13 +52,29 @@ def main():
             return True
         m = pat.search(n)
         return bool(m) and m.group(1) in modes
-    f_sel = [v for d, v in fetch.items() if keep(names[d])]
-    w_sel = [v for d, v in write.items() if keep(wnames[d])]
+    def select(per, nm):
+        """per-launch sums: kept gemm dispatches plus the splitk_reduce dispatch right after each one"""
+        out, last, nred = [], None, 0
+        for d in sorted(per, key=lambda x: int(x)):
+            n = nm[d]
+            if keep(n):
+                out.append(per[d])
+                last = len(out) - 1
+            elif "splitk_reduce" in n and last is not None:
+                out[last] += per[d]
+                nred += 1
+                last = None
+            else:
+                last = None
+        return out, nred
+    f_sel, f_red = select(fetch, names)
+    w_sel, w_red = select(write, wnames)
     if not f_sel or not w_sel:
         raise SystemExit("no matching dispatches")
     fetch_b = 2.0 * 1024 * sum(f_sel) / len(f_sel)   # gfx950: FETCH_SIZE counts half of wide reads
     write_b = 1024 * sum(w_sel) / len(w_sel)
     res = {"kernel": a.kernel, "mode": a.mode, "launches_fetch": len(f_sel), "launches_write": len(w_sel),
+           "splitk_reduce_dispatches": f_red,
            "fetch_bytes_per_launch": fetch_b, "write_bytes_per_launch": write_b,
            "bytes_per_launch": fetch_b + write_b,
            "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), WRITE_SIZE x1; KiB -> bytes",
