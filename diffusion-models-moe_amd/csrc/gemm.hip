@@ -1794,11 +1794,13 @@ extern "C" int sdmoe_mask_weight(const void* W, const void* bits, long N, long K
 
 int sdmoe_attn_set_nqf(int v);  // attention.hip
 int sdmoe_gn_set_fused(int v);  // norm.hip
+int sdmoe_gn_set_split(int v);  // norm.hip
 extern int g_topk_tpw;          // moe.hip
 
 extern "C" int sdmoe_tune(int knob, int value) {
   if (knob == 4) return sdmoe_attn_set_nqf(value);
   if (knob == 7) return sdmoe_gn_set_fused(value);
+  if (knob == 17) return sdmoe_gn_set_split(value);
   if (knob == 0 && (value == 0 || value == 2 || value == 3)) { g_stages = value; return SDMOE_OK; }
   if (knob == 1 && value >= 0 && value <= 8) { g_tile = value; return SDMOE_OK; }
   if (knob == 9 && value >= 0 && value <= 16) { g_ksplit = value; return SDMOE_OK; }
