@@ -336,279 +336,6 @@ __global__ __launch_bounds__(NW * 64, (D >= 160 || NW >= 8 ? 1 : 2)) void attn_f
 }
 
 // ---------------------------------------------------------------------------------------------------------------
-// attn_pp_kernel: attn_fwd_kernel's arithmetic (16x16x32, query on the lane, 8 waves x 32 queries, 64-key tiles) with
-// the two waves of every SIMD PING-PONGED. In attn_fwd_kernel all 8 waves run the same phase between the per-tile
-// barriers, so a SIMD's two waves issue their MFMAs (28 x 16 cycles per tile) and their softmax VALU (32 v_exp at 8
-// cycles + ~45 others at 4) at the same time and the two streams serialize: ~830 SIMD cycles per wave-tile against
-// ~450 for either alone (ISA count of attn_fwd_kernel<40,2,8,0>, r04). Here every tile is two segments,
-//   segment A (matrix): O^T += V^T P^T of the previous tile, then S^T = K Q~^T - m of this tile;
-//   segment B (vector): the online softmax of this tile -> P (fp16, registers);
-// and waves 4-7 run one segment behind waves 0-3, so between two barriers each SIMD holds one wave in A and one in B.
-// K and V have separate double buffers: K(kt) is read in the A segments of epochs 2 kt, 2 kt + 1, V(kt) in those of
-// 2 kt + 2, 2 kt + 3; both are fetched (LDS-DMA) during epochs 2 kt, 2 kt + 1 into the slots of K(kt - 1) / V(kt - 2).
-template <int D>
-__global__ __launch_bounds__(512, 1) void attn_pp_kernel(AttnParams p) {
-  constexpr int NQF = 2, NW = 8;
-  constexpr int DK = ((D + 31) / 32) * 32;
-  constexpr int DV = ((D + 15) / 16) * 16;
-  constexpr int KB = 64;
-  constexpr int RS = ((D + 15) / 16) % 2 ? ((D + 15) / 16) * 16 : ((D + 15) / 16) * 16 + 16;
-  constexpr int NDC = DK / 32, NDF = DV / 16;
-  constexpr int CH = D / 8;
-  constexpr int SL = RS / 8;
-  constexpr int TILE = KB * RS;
-  constexpr int NPIECE = TILE * 2 / 1024;
-  static_assert(NPIECE * 1024 == TILE * 2, "tiles must be whole 1-KiB pieces");
-  constexpr int NPW = (2 * NPIECE + NW - 1) / NW;
-  constexpr int KBUF = TILE + 64;
-  constexpr bool SUM_BY_MFMA = DV > D;
-  static_assert(!SUM_BY_MFMA || D % 16 == 8, "ones column sits at the start of a 4-column tr-read group");
-  constexpr float RESCALE_THR = 8.0f;
-  constexpr unsigned OOB = 0x80000000u;
-  __shared__ __attribute__((aligned(1024))) half_t KS0[KBUF];
-  __shared__ __attribute__((aligned(1024))) half_t KS1[KBUF];
-  __shared__ __attribute__((aligned(1024))) half_t VS0[TILE];
-  __shared__ __attribute__((aligned(1024))) half_t VS1[TILE];
-  __shared__ __attribute__((aligned(1024))) half_t ONES[SUM_BY_MFMA ? 16 * 16 : 1];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int grp = wave >> 2;  // waves w and w + 4 share SIMD w % 4
-  const int g = lane >> 4, w = lane & 15;
-  const int b = blockIdx.z, h = blockIdx.y;
-  const int q0 = blockIdx.x * (NW * 16 * NQF) + wave * (16 * NQF);
-
-  const half_t* Qb = p.Q + (long)b * p.Nq * p.ldq + h * D;
-  const half_t* Kb = p.K + (long)b * p.Nk * p.ldk + h * D;
-  const half_t* Vb = p.V + (long)b * p.Nk * p.ldv + h * D;
-  const __amdgpu_buffer_rsrc_t rsK =
-      __builtin_amdgcn_make_buffer_rsrc((void*)Kb, (short)0, (int)(((long)p.Nk - 1) * p.ldk * 2 + D * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsV =
-      __builtin_amdgcn_make_buffer_rsrc((void*)Vb, (short)0, (int)(((long)p.Nk - 1) * p.ldv * 2 + D * 2), 0x00020000);
-
-  // per-wave LDS-DMA pieces (global piece gp = wave + NW j: K pieces first, then V), offsets of tile 0
-  unsigned voff0[NPW], vstep[NPW];
-  int ldsoff[NPW];
-#pragma unroll
-  for (int j = 0; j < NPW; ++j) {
-    const int gp = wave + NW * j;
-    const bool isk = gp < NPIECE;
-    const int pc = isk ? gp : gp - NPIECE;
-    const int slot = pc * 64 + lane, r = slot / SL, c = slot - (slot / SL) * SL;
-    const long ld = isk ? p.ldk : p.ldv;
-    voff0[j] = c < CH ? (unsigned)(r * ld * 2 + c * 16) : OOB;
-    vstep[j] = (unsigned)(KB * ld * 2);
-    ldsoff[j] = pc * 512;
-  }
-  // K tile kk into Kd and V tile vk into Vd (either < 0: not issued)
-  auto issue = [&](int kk, int vk, half_t* Kd, half_t* Vd) __attribute__((always_inline)) {
-#pragma unroll
-    for (int j = 0; j < NPW; ++j) {
-      const int gp = wave + NW * j;  // wave-uniform
-      if (gp < NPIECE) {
-        if (kk >= 0) bld16(rsK, Kd + ldsoff[j], voff0[j] + (unsigned)kk * vstep[j]);
-      } else if (gp < 2 * NPIECE) {
-        if (vk >= 0) bld16(rsV, Vd + ldsoff[j], voff0[j] + (unsigned)vk * vstep[j]);
-      }
-    }
-  };
-
-  for (int i = tid; i < KBUF - TILE; i += NW * 64) KS0[TILE + i] = KS1[TILE + i] = 0;
-  if constexpr (SUM_BY_MFMA)
-    for (int i = tid; i < 16 * 16; i += NW * 64) ONES[i] = (half_t)(i % 16 == 8 ? 1.f : 0.f);
-
-  const int nkt = (p.Nk + KB - 1) / KB;
-  const bool ragged = (p.Nk % KB) != 0;
-  issue(0, -1, KS0, VS0);
-
-  half8 qf[NQF][NDC];
-#pragma unroll
-  for (int f = 0; f < NQF; ++f)
-#pragma unroll
-    for (int c = 0; c < NDC; ++c) {
-      const int q = q0 + f * 16 + w, d = 32 * c + 8 * g;
-      half8 v = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (q < p.Nq && d < D) v = *reinterpret_cast<const half8*>(Qb + (long)q * p.ldq + d);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (half_t)((float)v[j] * p.scale_log2);
-      qf[f][c] = v;
-    }
-
-  float4v oacc[NQF][NDF];
-#pragma unroll
-  for (int f = 0; f < NQF; ++f)
-#pragma unroll
-    for (int d = 0; d < NDF; ++d) oacc[f][d] = (float4v){0.f, 0.f, 0.f, 0.f};
-  float mrun[NQF], lrun[NQF];
-#pragma unroll
-  for (int f = 0; f < NQF; ++f) mrun[f] = lrun[f] = 0.f;
-  float4v s[NQF][4];
-  half8 pb[NQF][2];
-
-  const int tq = w >> 2, tp = w & 3;
-  auto vaddr = [&](const half_t* Vt, int c2, int hi, int df) __attribute__((always_inline)) -> const half_t* {
-    const int normal = (32 * c2 + 16 * hi + 4 * g + tq) * RS + 16 * df + 4 * tp;
-    if (SUM_BY_MFMA && df == D / 16 && 4 * tp == D % 16) return ONES + (4 * g + tq) * 16 + 8;
-    return Vt + normal;
-  };
-
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  // segment A of tile kt: PV of tile kt - 1 (V slot VP), QK of tile kt (K slot KP)
-  auto seg_a = [&](int kt, auto kp_tag) __attribute__((always_inline)) {
-    constexpr int KP = decltype(kp_tag)::value;
-    const half_t* Kt = KP ? KS1 : KS0;
-    const half_t* Vt = KP ? VS0 : VS1;  // tile kt - 1 has the other parity
-    if (kt > 0) {
-#pragma unroll
-      for (int c2 = 0; c2 < 2; ++c2)
-#pragma unroll
-        for (int df = 0; df < NDF; ++df) {
-          const half4 lo = ds_read_tr(vaddr(Vt, c2, 0, df));
-          const half4 hi = ds_read_tr(vaddr(Vt, c2, 1, df));
-          const half8 a = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-#pragma unroll
-          for (int f = 0; f < NQF; ++f) oacc[f][df] = mfma16x16x32(a, pb[f][c2], oacc[f][df]);
-        }
-    }
-    if (kt < nkt) {
-#pragma unroll
-      for (int f = 0; f < NQF; ++f) {
-        const float nm = -mrun[f];
-#pragma unroll
-        for (int kf = 0; kf < 4; ++kf) s[f][kf] = (float4v){nm, nm, nm, nm};
-      }
-#pragma unroll
-      for (int kf = 0; kf < 4; ++kf)
-#pragma unroll
-        for (int c = 0; c < NDC; ++c) {
-          const half8 a = *reinterpret_cast<const half8*>(Kt + (kf * 16 + w) * RS + 32 * c + 8 * g);
-#pragma unroll
-          for (int f = 0; f < NQF; ++f) s[f][kf] = mfma16x16x32(a, qf[f][c], s[f][kf]);
-        }
-    }
-  };
-
-  // segment B of tile kt: online softmax (attn_fwd_kernel's, deferred rescale) -> pb
-  auto seg_b = [&](int kt) __attribute__((always_inline)) {
-    if (kt >= nkt) return;
-#pragma unroll
-    for (int f = 0; f < NQF; ++f) {
-      if (ragged && kt == nkt - 1) {
-#pragma unroll
-        for (int kf = 0; kf < 4; ++kf)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (kt * KB + kf * 16 + 4 * g + i >= p.Nk) s[f][kf][i] = -INFINITY;
-      }
-      float m0 = max3(s[f][0][0], s[f][0][1], s[f][0][2]);
-      float m1 = max3(s[f][0][3], s[f][1][0], s[f][1][1]);
-      float m2 = max3(s[f][1][2], s[f][1][3], s[f][2][0]);
-      float m3 = max3(s[f][2][1], s[f][2][2], s[f][2][3]);
-      float m4 = max3(s[f][3][0], s[f][3][1], s[f][3][2]);
-      m0 = max3(m0, m1, s[f][3][3]);
-      m2 = max3(m2, m3, m4);
-      const float ml = max2(m0, m2);
-      if (kt == 0) {
-        const float mx = max_xrows(ml);
-        mrun[f] = mx;
-#pragma unroll
-        for (int kf = 0; kf < 4; ++kf) s[f][kf] -= mx;
-      } else if (!__all(ml <= RESCALE_THR)) {
-        const float delta = fmaxf(max_xrows(ml), 0.f);
-        mrun[f] += delta;
-        const float alpha = __builtin_amdgcn_exp2f(-delta);
-        if (!SUM_BY_MFMA) lrun[f] *= alpha;
-#pragma unroll
-        for (int d = 0; d < NDF; ++d) oacc[f][d] *= alpha;
-#pragma unroll
-        for (int kf = 0; kf < 4; ++kf) s[f][kf] -= delta;
-      }
-      float ls = 0.f;
-#pragma unroll
-      for (int kf = 0; kf < 4; ++kf)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float e = __builtin_amdgcn_exp2f(s[f][kf][i]);
-          s[f][kf][i] = e;
-          if (!SUM_BY_MFMA) ls += e;
-        }
-      if (!SUM_BY_MFMA) lrun[f] += ls;
-#pragma unroll
-      for (int c2 = 0; c2 < 2; ++c2) {
-        half8 v;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          v[i] = (half_t)s[f][2 * c2][i];
-          v[4 + i] = (half_t)s[f][2 * c2 + 1][i];
-        }
-        pb[f][c2] = v;
-      }
-    }
-  };
-
-  // one epoch: the group-local step ls = e - grp; residue LR = ls mod 4 (compile-time): 0 / 2 = segment A of an
-  // even / odd tile, 1 / 3 = segment B
-  auto step = [&](int ls, auto lr_tag) __attribute__((always_inline)) {
-    constexpr int LR = decltype(lr_tag)::value;
-    if (ls < 0) return;
-    if constexpr (LR % 2 == 0) seg_a(ls >> 1, std::integral_constant<int, LR / 2>());
-    else seg_b(ls >> 1);
-  };
-  auto epoch = [&](int e, auto r_tag) __attribute__((always_inline)) {
-    constexpr int R = decltype(r_tag)::value;
-    if constexpr (R % 2 == 0) {  // e = 2 kt: fetch K(kt + 1) and V(kt) into the slots freed by the last barrier
-      const int kt = e >> 1;
-      issue(kt + 1 < nkt ? kt + 1 : -1, kt < nkt ? kt : -1, R / 2 ? KS0 : KS1, R / 2 ? VS1 : VS0);
-    }
-    if (grp == 0) step(e, std::integral_constant<int, R>());
-    else step(e - 1, std::integral_constant<int, (R + 3) & 3>());
-    if constexpr (R % 2 == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  };
-  using R0 = std::integral_constant<int, 0>;
-  using R1 = std::integral_constant<int, 1>;
-  using R2 = std::integral_constant<int, 2>;
-  using R3 = std::integral_constant<int, 3>;
-  const int E = 2 * nkt + 2;  // group 1 finishes one epoch after group 0
-  for (int e = 0; e < E; e += 4) {
-    epoch(e, R0());
-    epoch(e + 1, R1());
-    if (e + 2 < E) {
-      epoch(e + 2, R2());
-      epoch(e + 3, R3());
-    }
-  }
-
-  half_t* Ob = p.O + (long)b * p.Nq * p.ldo + h * D;
-#pragma unroll
-  for (int f = 0; f < NQF; ++f) {
-    float l;
-    if (SUM_BY_MFMA) {
-      l = __shfl(oacc[f][D / 16][D % 4], ((D % 16) / 4) * 16 + w, 64);
-    } else {
-      l = lrun[f];
-      l += __shfl_xor(l, 16, 64);
-      l += __shfl_xor(l, 32, 64);
-    }
-    const float inv = 1.0f / l;
-    const int q = q0 + f * 16 + w;
-    if (q >= p.Nq) continue;
-#pragma unroll
-    for (int df = 0; df < NDF; ++df) {
-      const int d = 16 * df + 4 * g;
-      if (d < D) {
-        half4 o;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) o[i] = (half_t)(oacc[f][df][i] * inv);
-        *reinterpret_cast<half4*>(Ob + (long)q * p.ldo + d) = o;
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------------------------------
 // attn32_kernel: the same flash-style forward on v_mfma_f32_32x32x16_f16, both products with the QUERY ON THE LANE:
 //   S^T (32 keys x 32 queries per MFMA block) = K Q^T   -- A = K rows from LDS (ds_read_b128), B = Q^T in registers;
 //   O^T (32 d x 32 queries)                   = V^T P^T -- A = V^T by ds_read_b64_tr_b16, B = P^T straight from the
@@ -907,10 +634,7 @@ int launch(const AttnParams& p, int nimg, hipStream_t s) {
   // self-attentions at d = 40 / 64: d = 40 N = 4096 448 vs 464-475 us, pipeline +0.5 % (same box); slower on the
   // 77-key cross-attention (34.4 vs 31.1 us: fewer workgroups) and at d = 80 (65.4 vs 62.4 us with attn32)
   const bool use8 = g_attn_nqf == 8 || (g_attn_nqf == 0 && (D == 40 || D == 64) && p.Nk > 128);
-  if (g_attn_nqf == 32 && D <= 80) {
-    dim3 grid((p.Nq + 255) / 256, p.heads, nimg);
-    attn_pp_kernel<(D <= 80 ? D : 40)><<<grid, 512, 0, s>>>(p);
-  } else if (use32) {
+  if (use32) {
     dim3 grid((p.Nq + 127) / 128, p.heads, nimg);
     attn32_kernel<D><<<grid, 256, 0, s>>>(p);
   } else if (WIDE_OK && wide) {
@@ -936,7 +660,7 @@ int launch(const AttnParams& p, int nimg, hipStream_t s) {
 }  // namespace
 
 int sdmoe_attn_set_nqf(int v) {
-  if (v != 0 && v != 1 && v != 2 && v != 4 && v != 8 && v != 16 && v != 32 && v != 40) return SDMOE_EARG;
+  if (v != 0 && v != 1 && v != 2 && v != 4 && v != 8 && v != 16 && v != 40) return SDMOE_EARG;
   g_attn_nqf = v;
   return SDMOE_OK;
 }
