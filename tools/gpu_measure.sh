@@ -45,14 +45,16 @@ for s in $STEPS; do
       step $s 600 rocprofv3 --kernel-trace --stats -d $O/$s -o run --output-format csv -- python3 $R/bench.py $args $BA
       cd $R
       f=$(find $O/$s -name '*kernel_stats.csv' 2>/dev/null | head -1)
-      [ -n "$f" ] && python tools/prof_summary.py $f 45 > $O/${s}_summary.txt && head -14 $O/${s}_summary.txt ;;
+      [ -n "$f" ] && python tools/prof_summary.py $f 45 > $O/${s}_summary.txt && cp $f $O/${s}_kernel_stats.csv && head -14 $O/${s}_summary.txt
+      rm -rf $O/$s ;;  # the raw traces would push gpurun_out past the 64 MiB copy-back limit
     pmc)
       cd /tmp && export TMPDIR=/tmp
       for c in FETCH_SIZE WRITE_SIZE; do
         timeout -s KILL 300 rocprofv3 --pmc $c -d $O/pmc_$c -o run --output-format csv -- python3 $R/bench.py --inference-steps 2 --steps 1 --warmup 0 --no-cpu-baseline --no-roofline --e2e-steps 0 > $O/pmc_$c.log 2>&1 || { echo "pmc $c failed"; exit 1; }
       done
       cd $R
-      python tools/pmc_traffic.py $(find $O/pmc_FETCH_SIZE -name '*counter_collection.csv' | head -1) $(find $O/pmc_WRITE_SIZE -name '*counter_collection.csv' | head -1) --out $O/pmc_conv_traffic.json --build "$(cat $R/.build_rev 2>/dev/null)" ;;
+      python tools/pmc_traffic.py $(find $O/pmc_FETCH_SIZE -name '*counter_collection.csv' | head -1) $(find $O/pmc_WRITE_SIZE -name '*counter_collection.csv' | head -1) --out $O/pmc_conv_traffic.json --build "$(cat $R/.build_rev 2>/dev/null)"
+      for c in FETCH_SIZE WRITE_SIZE; do gzip -c $(find $O/pmc_$c -name '*counter_collection.csv' | head -1) > $O/pmc_$c.csv.gz; rm -rf $O/pmc_$c; done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
