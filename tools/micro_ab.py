@@ -18,6 +18,9 @@ DEV = "cuda"
 N_IMG = 16
 
 
+DEFAULTS = {"7": 1, "8": 1, "14": 1, "16": 1}  # sdmoe_tune knobs whose default is not 0
+
+
 def rnd(*shape, scale=1.0):
     return (torch.randn(*shape, device=DEV) * scale).half()
 
@@ -31,6 +34,9 @@ def gn_cases():
         y = torch.empty_like(x)
         out.append((f"groupnorm+silu HW={HW} C={C}", lambda x=x, g=g, b=b, y=y, HW=HW:
                     ops.groupnorm(x, N_IMG, HW, g, b, 1e-5, 32, True, out=y), 3 * x.numel() * 2, "B"))
+        if HW > 256:
+            out.append((f"groupnorm stats HW={HW} C={C}", lambda x=x, g=g, b=b, HW=HW:
+                        ops.groupnorm_stats(x, N_IMG, HW, g, b, 1e-5, 32), x.numel() * 2, "B"))
     return out
 
 
@@ -143,7 +149,7 @@ def main():
             r = run(cases, a.iters)
             for kv in filter(None, st.split(",")):  # back to defaults (0) unless the knob's default differs
                 k, _ = kv.split("=")
-                _lib.check(lib.sdmoe_tune(int(k), 1 if k in ("7", "8", "14") else 0), "tune")
+                _lib.check(lib.sdmoe_tune(int(k), DEFAULTS.get(k, 0)), "tune")
             for name, v in r.items():
                 table.setdefault(name, {}).setdefault(st, []).append(v)
     for name, per in table.items():
