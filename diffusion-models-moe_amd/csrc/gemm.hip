@@ -62,7 +62,7 @@ struct GemmParams {
   int kchunk2;  // halo conv: folded-shortcut K-steps (32 channels of A2 each) per split (kchunk = main slices per split)
   int mfast;  // tile order M-fastest (split-K grids, sdmoe_tune knob 14)
   int a_bytes, w_bytes;  // SRD num_records
-  // routed-GEGLU epilogue (sdmoe_linear_geglu): W rows interleaved [value 8 | gate 8] per 8-neuron chunk, C is
+  // routed-GEGLU epilogue (sdmoe_linear_geglu): W rows interleaved [value 2 | gate 2] per neuron pair, C is
   // the [M, N/2] product value * act(gate); score [M, ld_score] gets per-expert sums of act(gate) over
   // contiguous esize-neuron experts (neurons pre-permuted so every expert is contiguous)
   half_t* score; long ld_score;
@@ -989,14 +989,14 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
     int lane_o = lane;
     asm volatile("" : "+v"(lane_o));
     const int fr_e = lane_o & 15, fg_e = lane_o >> 4;
-    // Routed GEGLU on the swapped fragments, value and gate paired in registers: lane (fr, fg) holds columns
-    // 16 j + 4 fg .. +3 of row 16 i + fr, i.e. values of 4 neurons (fg 0/1) or their gates (fg 2/3, lane + 32).
-    // Two v_permlane32_swap per fragment leave lane (fr, fg) with value and gate of neurons 8 j + nsel, +1
-    // (nsel = 0, 4, 2, 6 for fg = 0..3). The fp16 product and the activated gate (both exact fp16 values) are
-    // staged in LDS per wave ([RG rows][NH neurons] each; the 16 rows x 4 lanes of a 4-B store phase hit 64
-    // distinct banks at NH = 40), then copied out as 16-B row chunks, and every (row, expert) lane sums its
-    // expert's gates in neuron order in fp32 -- the rounding points of sdmoe_linear + sdmoe_geglu_route (bit-
-    // identical). LDS traffic per wave tile: 4 x WM x NH x 2 B, a quarter of staging fp32 accumulators and bias.
+    // Routed GEGLU on the swapped fragments, value and gate paired in registers by the weight layout: lane
+    // (fr, fg) holds columns 16 j + 4 fg .. +3 of row 16 i + fr, i.e. [value, value, gate, gate] of neurons
+    // 8 j + 2 fg, +1 (W rows interleaved [v 2 | g 2] per neuron pair: no cross-lane move; the [v 8 | g 8] layout
+    // of rounds 1-3 needed two v_permlane32_swap per fragment, 2 of its 11 epilogue instructions). The fp16
+    // product and the activated gate (both exact fp16 values) are staged in LDS per wave ([RG rows][NH neurons]
+    // each; the 16 rows x 4 lanes of a 4-B store phase hit 64 distinct banks at NH = 40), then copied out as 16-B
+    // row chunks, and every (row, expert) lane sums its expert's gates in neuron order in fp32 -- the rounding
+    // points of sdmoe_linear + sdmoe_geglu_route (bit-identical). LDS traffic per wave tile: 4 x WM x NH x 2 B.
     typedef _Float16 h2 __attribute__((ext_vector_type(2)));
     constexpr int NH = WN / 2;                    // neurons of this wave's tile
     constexpr int FPP = FM % 2 == 0 ? 2 : 1;      // fragment rows per staging pass
@@ -1025,18 +1025,17 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const int nsel = (fg_e & 1) * 4 + (fg_e >> 1) * 2;
+    const int nsel = 2 * fg_e;  // this lane's neuron pair in every fragment: 8 j + nsel, +1
     constexpr int CPO = NH / 8, RPI = 64 / CPO;  // copy-out: 16-B chunks per staged row, rows per 64-lane round
     const int lr = lane_o / CPO, lc = lane_o - (lane_o / CPO) * CPO;
     half_t* const cout = p.C + (long)(mw + lr) * p.ldc + nw / 2 + 8 * lc;
-    // this lane's bias pairs in every fragment (value cols 16 j + nsel, +1; gate cols +8), hoisted out of the rows
-    // (the table GELU's epilogue reads them from LDS per fragment instead: its temporaries need those 20 VGPRs)
-    float2v bvv[FN], bgg[FN];
+    // this lane's bias quads in every fragment (columns 16 j + 4 fg .. +3: value, value, gate, gate), hoisted out
+    // of the rows (the table GELU's epilogue reads them from LDS per fragment instead: its temporaries need those
+    // 20 VGPRs)
+    float4v bq[FN];
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      bvv[j] = gtab ? (float2v){0.f, 0.f} : *reinterpret_cast<const float2v*>(gbias + 16 * j + nsel);
-      bgg[j] = gtab ? (float2v){0.f, 0.f} : *reinterpret_cast<const float2v*>(gbias + 16 * j + 8 + nsel);
-    }
+    for (int j = 0; j < FN; ++j)
+      bq[j] = gtab ? (float4v){0.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const float4v*>(gbias + 16 * j + 4 * fg_e);
     auto stage_pass = [&](int h, auto act_tag) {
       constexpr int ACTK = decltype(act_tag)::value;  // 0: ReLU, 1: GELU from the LDS table, 2: apply_act
       constexpr bool RELU = ACTK == 0;
@@ -1057,12 +1056,9 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = __builtin_fmaf(la, v[r], lc * ws[r]);
           }
-          const auto s02 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[0]), __float_as_uint(v[2]), false, false);
-          const auto s13 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[1]), __float_as_uint(v[3]), false, false);
-          const float2v bv = ACTK == 1 ? *reinterpret_cast<const float2v*>(gbias + 16 * j + nsel) : bvv[j];
-          const float2v bg = ACTK == 1 ? *reinterpret_cast<const float2v*>(gbias + 16 * j + 8 + nsel) : bgg[j];
-          const h2 yv = {(half_t)(__uint_as_float(s02[0]) + bv[0]), (half_t)(__uint_as_float(s13[0]) + bv[1])};
-          const h2 yg = {(half_t)(__uint_as_float(s02[1]) + bg[0]), (half_t)(__uint_as_float(s13[1]) + bg[1])};
+          const float4v b = ACTK == 1 ? *reinterpret_cast<const float4v*>(gbias + 16 * j + 4 * fg_e) : bq[j];
+          const h2 yv = {(half_t)(v[0] + b[0]), (half_t)(v[1] + b[1])};
+          const h2 yg = {(half_t)(v[2] + b[2]), (half_t)(v[3] + b[3])};
           h2 ga;
           if constexpr (RELU) ga = __builtin_elementwise_max(yg, (h2){(half_t)0.f, (half_t)0.f});
           else if constexpr (ACTK == 1) ga = (h2){gelu_tab_h(yg[0], tab), gelu_tab_h(yg[1], tab)};

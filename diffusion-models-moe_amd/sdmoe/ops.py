@@ -505,16 +505,18 @@ class Routing:
 
 
 def interleave_geglu(weight: torch.Tensor, bias: torch.Tensor | None, perm: torch.Tensor | None):
-    """proj.weight [2F, K] (value rows, then gate rows) -> rows permuted by `perm` and interleaved [v 8 | g 8]
-    per 8 neurons, the layout sdmoe_linear_geglu reads. bias likewise (zeros if None)."""
+    """proj.weight [2F, K] (value rows, then gate rows) -> rows permuted by `perm` and interleaved [v 2 | g 2]
+    per neuron pair (rows 4 q .. 4 q + 3 = value 2q, value 2q+1, gate 2q, gate 2q+1), the layout sdmoe_linear_geglu
+    reads: each lane of its swapped MFMA fragments then holds both halves of two neurons. bias likewise (zeros if
+    None)."""
     F2, K = weight.shape
     F = F2 // 2
     idx = torch.arange(F, device=weight.device) if perm is None else perm.to(weight.device)
     wv, wg = weight[:F][idx], weight[F:][idx]
-    w_il = torch.stack([wv.view(F // 8, 8, K), wg.view(F // 8, 8, K)], 1).reshape(F2, K).contiguous()
+    w_il = torch.stack([wv.view(F // 2, 2, K), wg.view(F // 2, 2, K)], 1).reshape(F2, K).contiguous()
     b = torch.zeros(F2, dtype=weight.dtype, device=weight.device) if bias is None else bias
     bv, bg = b[:F][idx], b[F:][idx]
-    b_il = torch.stack([bv.view(F // 8, 8), bg.view(F // 8, 8)], 1).reshape(F2).contiguous()
+    b_il = torch.stack([bv.view(F // 2, 2), bg.view(F // 2, 2)], 1).reshape(F2).contiguous()
     return w_il, b_il
 
 
@@ -523,7 +525,7 @@ def interleave_ln_fold(fold: LNFold, perm: torch.Tensor | None) -> LNFold:
     F = fold.w.shape[0] // 2
     dev = fold.w.device
     idx = torch.arange(F, device=dev) if perm is None else perm.to(dev)
-    rows = torch.stack([idx.view(F // 8, 8), (idx + F).view(F // 8, 8)], 1).reshape(2 * F)
+    rows = torch.stack([idx.view(F // 2, 2), (idx + F).view(F // 2, 2)], 1).reshape(2 * F)
     return fold.rows(rows)
 
 

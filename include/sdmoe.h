@@ -186,7 +186,7 @@ int sdmoe_geglu_route(const void* Y, long ldy, int M, int F, int E, int k, int a
  *  1. sdmoe_linear_geglu: P[m, n] = fp16(fp16(x W_v^T + b_v) * fp16(act(fp16(x W_g^T + b_g)))) for all F neurons
  *     and score[m, e] = fp16(sum over expert e's neurons of act(gate)) in the GEMM epilogue. W [2F, K] / bias
  *     [2F] hold the neurons permuted so every expert is contiguous (expert-major, ascending neuron id), value
- *     and gate rows interleaved in chunks of 8 ([v 8 | g 8] per 8 neurons). F % 80 == 0. score may be NULL
+ *     and gate rows interleaved in pairs ([v 2 | g 2] per neuron pair). F % 80 == 0. score may be NULL
  *     (dense GEGLU). Same rounding points as sdmoe_linear + sdmoe_geglu_route.
  *  2. sdmoe_moe_topk_mask: per token, removed experts score 0, top-k (ties toward the lowest expert id) and
  *     zero every neuron of P whose expert is not selected or removed. sel_out as above (may be NULL).

@@ -437,7 +437,7 @@ def test_initial_latents_unseeded_process_seed():
 
 def test_interleave_ln_fold_matches_geglu_interleave():
     """The LayerNorm fold's rows (folded weight, fp32 bias, row sums) are reordered exactly like interleave_geglu
-    reorders the projection's rows, so sdmoe_linear_geglu_ln sees the same [value 8 | gate 8] expert-major layout."""
+    reorders the projection's rows, so sdmoe_linear_geglu_ln sees the same [value 2 | gate 2] expert-major layout."""
     from sdmoe import ops
     F, K = 160, 64
     g = torch.Generator().manual_seed(3)
