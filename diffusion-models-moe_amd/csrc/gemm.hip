@@ -1280,6 +1280,11 @@ int try_halo(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
   return -1;
 }
 
+// knob 20: 1 (default) = the table-GELU GEGLU on the 256x320 2x4-wave tiles like the ReLU one (no scratch since the
+// [v 2 | g 2] layout: 150.9-154.3 vs 178.2-186.2 us at M = 16384, C = 640; SDXL pipeline +4.0 %, same box);
+// 0 = 256x160 4x2 tiles (rounds 3-4 until the layout change: 364 B/lane of scratch on 256x320)
+int g_gt320 = 1;
+
 // routed-GEGLU linear: BN in {160, 320} tiles only (wave tile width 80 = 40 neurons = whole experts), no split-K
 template <int MODE>
 int dispatch_geglu(const GemmParams& p, hipStream_t s) {
@@ -1289,9 +1294,8 @@ int dispatch_geglu(const GemmParams& p, hipStream_t s) {
   if (g_tile == 4) return launch_tile<256, 160, 4, 2, MODE>(p, nullptr, 0, s);
   if constexpr (MODE != MODE_GEGLU_GT)  // (no room for the GELU table behind that tile's staging)
     if (g_tile == 7) return launch_tile<128, 160, 4, 2, MODE>(p, nullptr, 0, s);  // sweep: two workgroups per CU
-  if (MODE == MODE_GEGLU_GT && g_tile == 0 && p.N % 320 == 0 && nt320 >= 240)
-    // the table-GELU epilogue does not fit 256x320's registers next to the 160 accumulators (scratch in the K loop):
-    // the same rows on 256x160 tiles, 8 waves 4 x 2 (wave tile 64 x 80)
+  if (MODE == MODE_GEGLU_GT && g_tile == 0 && !g_gt320 && p.N % 320 == 0 && nt320 >= 240)
+    // knob 20 = 0: the same rows on 256x160 tiles, 8 waves 4 x 2 (wave tile 64 x 80)
     return launch_tile<256, 160, 4, 2, MODE>(p, nullptr, 0, s);
   if (p.N % 320 == 0 && nt320 >= 240) {
     // 2x4 waves (wave tile 128 rows x 40 neurons): with the row-fastest epilogue its 32-row staging passes are
@@ -1807,5 +1811,6 @@ extern "C" int sdmoe_tune(int knob, int value) {
   if (knob == 8 && (value == 0 || value == 1)) { g_res16 = value; return SDMOE_OK; }
   if (knob == 15 && (value == 0 || value == 1 || value == 4)) { g_topk_tpw = value; return SDMOE_OK; }
   if (knob == 16 && value >= 0 && value <= 3) { g_halo = value; return SDMOE_OK; }
+  if (knob == 20 && (value == 0 || value == 1)) { g_gt320 = value; return SDMOE_OK; }
   return SDMOE_EARG;
 }

@@ -350,8 +350,9 @@ def test_topk_keep_quad_kernel(M, E, k, nrem, esize, ld):
     assert np.array_equal(bits.transpose(1, 0, 2).reshape(M, F), neur)
 
 
-@pytest.mark.parametrize("M", [64, 4096, 8192])  # 64x160 (table loaded after the K loop), 128x160, 256x320 tiles
-def test_gelu_every_fp16_input_matches_reference_activation(M):
+# 64x160 (table loaded after the K loop), 128x160, 256x160 4x2 (knob 20 = 0) / 256x320 2x4 (default at M = 8192) tiles
+@pytest.mark.parametrize("M,gt320", [(64, 0), (4096, 0), (8192, 0), (8192, 1)])
+def test_gelu_every_fp16_input_matches_reference_activation(M, gt320):
     """The GEGLU kernels' GELU on EVERY finite fp16 gate value vs the reference's activation itself (F.gelu on an fp16
     tensor: diffusers GEGLU.gelu, the hook's module.gelu(gate), moefy.py:13): sdmoe_geglu_route (gate_out) and the
     fused routed-GEGLU epilogue (value 1.0, so P = gelu(gate)) are bit-identical to it on all but <= 2 inputs (the fp32
@@ -375,7 +376,13 @@ def test_gelu_every_fp16_input_matches_reference_activation(M):
     x[torch.arange(M), torch.arange(M) % 64] = 1.0
     w = torch.cat([torch.ones(F, 64, dtype=torch.float16), gate.t().contiguous()], 0).to(DEV)
     w_il, b_il = ops.interleave_geglu(w, torch.zeros(2 * F, dtype=torch.float16, device=DEV), None)
-    P = ops.linear_geglu(x.to(DEV), w_il, b_il, ops.ACT_GELU).cpu()
+    from sdmoe import _lib
+    lib = _lib.load()
+    _lib.check(lib.sdmoe_tune(20, gt320), "tune")
+    try:
+        P = ops.linear_geglu(x.to(DEV), w_il, b_il, ops.ACT_GELU).cpu()
+    finally:
+        _lib.check(lib.sdmoe_tune(20, 1), "tune")
     exp_rows = torch.arange(M) % 64
     assert torch.equal(P, got_u[exp_rows])                    # fused == unfused, bit for bit
     same = (got_u.view(torch.int16) == ref.view(torch.int16)) | ((got_u == 0) & (ref == 0))
