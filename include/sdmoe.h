@@ -359,8 +359,13 @@ int sdmoe_cfg_multistep_step(const void* eps, long lde, float* lat, int B, int H
    registers, 2 the same launch re-reading the rows for the apply, 0 two launches;
    knob 8 = GEMM residual epilogue: 1 (default) output rounded to fp16 then the residual added in fp16 arithmetic
    (diffusers' fp16 `linear(x) + residual`), 0 = accumulator + residual rounded once (fp32 staging);
-   knob 15 = top-k expert selection kernels: 0 (default) one token per wave at M <= 16384, four above; 1 / 4 = always
-   one / four tokens per wave. */
+   knob 15 = top-k expert selection kernels: 0 (default) one token per wave at M <= 16384, four above, and the keep
+   bits at E <= 64 with one quad of lanes per token; 1 / 4 = always the ballot kernel at one / four tokens per wave;
+   knob 16 = halo-tiled 3x3 convs: 1 (default) where measured faster (64- and 16-wide outputs, the upsample convs),
+   2 = every 128-row halo tile instead, 3 = the default plus 32-wide outputs on 256-row tiles, 0 = off;
+   knob 17 = sdmoe_groupnorm above 256 positions: 0 (default) statistics kernels + apply, 1 = wide slice sums +
+   one finalize-and-apply launch;
+   knob 20 = table-GELU routed GEGLU tiles: 1 (default) 256x320 like the ReLU kernel, 0 = 256x160 (4x2 waves). */
 int sdmoe_tune(int knob, int value);
 
 /*
