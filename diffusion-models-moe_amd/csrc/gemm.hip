@@ -1226,7 +1226,7 @@ int launch_halo(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
   const int nsl = p.Cin / 32;
   int ksplit = 1;
   if (ws && ntiles < 200) {
-    ksplit = (256 + ntiles - 1) / ntiles;
+    ksplit = (256 + ntiles - 1) / ntiles;  // 6 / 8 splits: 172 vs 128 us at 16x16 x 1280 (r04)
     if (ksplit > 8) ksplit = 8;
     if (ksplit > nsl / 2) ksplit = nsl / 2;
     while (ksplit > 1 && (long)ksplit * p.M * p.N > ws_floats) --ksplit;
@@ -1361,6 +1361,13 @@ int dispatch(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
     if (p.stride == 1 && p.N % 320 == 0 && nt320 < 240 && p.K >= 9 * 1280 && p.M >= 2048 && p.M <= 4096)
       return launch_tile<256, 320, 2, 4, MODE>(p, ws, ws_floats, s);
     if (p.stride == 2 && p.N % 160 == 0 && p.M >= 8192) return launch_tile<64, 160, 2, 2, MODE>(p, ws, ws_floats, s);
+    // the 32x32 -> 16x16 and 16x16 -> 8x8 downsamplers (M = 4096 / 1024): a 4-way split-K, two workgroups per CU
+    // (their strided-tap A loads want the extra waves in flight): 46.1-46.7 vs 65.7-66.3 us and 46.4-46.9 vs
+    // 78.4-80.1 us with the auto ~one-per-CU split of 2, on every tile shape (same box)
+    if (p.stride == 2 && p.N % 160 == 0 && p.M < 8192) {
+      if (p.M > 2048) return launch_tile<128, 160, 2, 2, MODE>(p, ws, ws_floats, s, 4);
+      return launch_tile<64, 160, 2, 2, MODE>(p, ws, ws_floats, s, 4);
+    }
   }
   if (p.N % 160 == 0 && p.K >= 2560 && nt160_128 < 300 && !(MODE == MODE_CONV && p.stride == 2))
     return launch_tile<256, 160, 4, 2, MODE>(p, ws, ws_floats, s);
