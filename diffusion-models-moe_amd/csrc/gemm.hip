@@ -1284,6 +1284,7 @@ int try_halo(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
 // [v 2 | g 2] layout: 150.9-154.3 vs 178.2-186.2 us at M = 16384, C = 640; SDXL pipeline +4.0 %, same box);
 // 0 = 256x160 4x2 tiles (rounds 3-4 until the layout change: 364 B/lane of scratch on 256x320)
 int g_gt320 = 1;
+int g_narrow = 0;  // knob 21: 1 = N <= 32 outputs (conv_out's 8 padded channels) on 128x32 tiles, 0 = 128x64
 
 // routed-GEGLU linear: BN in {160, 320} tiles only (wave tile width 80 = 40 neurons = whole experts), no split-K
 template <int MODE>
@@ -1375,6 +1376,8 @@ int dispatch(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
     if (p.N % 160 == 0) return launch_tile<128, 160, 2, 2, MODE>(p, ws, ws_floats, s);
     return launch_tile<128, 128, 2, 2, MODE>(p, ws, ws_floats, s);
   }
+  if constexpr (MODE == MODE_CONV)  // conv_out (N = 8 padded channels): a quarter of 128x64's MFMA padding
+    if (p.N <= 32 && g_narrow) return launch_tile<128, 32, 2, 2, MODE>(p, ws, ws_floats, s);
   if (p.N <= 64) return launch_tile<128, 64, 2, 2, MODE>(p, ws, ws_floats, s);
   if (p.N % 160 == 0) {
     if (nt160_128 >= 200 || p.M > 2048) return launch_tile<128, 160, 2, 2, MODE>(p, ws, ws_floats, s);
@@ -1819,5 +1822,6 @@ extern "C" int sdmoe_tune(int knob, int value) {
   if (knob == 15 && (value == 0 || value == 1 || value == 4)) { g_topk_tpw = value; return SDMOE_OK; }
   if (knob == 16 && value >= 0 && value <= 3) { g_halo = value; return SDMOE_OK; }
   if (knob == 20 && (value == 0 || value == 1)) { g_gt320 = value; return SDMOE_OK; }
+  if (knob == 21 && (value == 0 || value == 1)) { g_narrow = value; return SDMOE_OK; }
   return SDMOE_EARG;
 }

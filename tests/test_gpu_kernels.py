@@ -369,6 +369,8 @@ def _with_tune(settings, fn):
         _lib.check(lib.sdmoe_tune(0, 0), "tune")
         _lib.check(lib.sdmoe_tune(1, 0), "tune")
         _lib.check(lib.sdmoe_tune(16, 1), "tune")
+        _lib.check(lib.sdmoe_tune(20, 1), "tune")
+        _lib.check(lib.sdmoe_tune(21, 0), "tune")
 
 
 # tiles (sdmoe_tune knob 1): 0 auto, 1 = 128x160, 2 = 64x160, 3 = 256x320 (2x4 waves), 4 = 256x160 (4x2), 5 = 256x320
@@ -433,6 +435,18 @@ def test_conv3x3_halo_tiles(H, Cin, Cout, nimg, up):
         close(o, ref)
     for o in outs[:3]:
         close(o, outs[3].float())
+
+
+@pytest.mark.parametrize("Cout,narrow", [(8, 1), (8, 0), (16, 1), (32, 1), (24, 1)])
+def test_conv3x3_narrow_outputs(Cout, narrow):
+    """conv_out's shape (320 -> 8 padded channels at 64x64) on the 128x32 tile (sdmoe_tune knob 21 = 1, default) and on
+    128x64 (0): vs torch fp32, bias and an M tail (3 images of 10x10)."""
+    for nimg, H, Cin in [(2, 64, 320), (3, 10, 128)]:
+        x = rnd(nimg * H * H, Cin, seed=Cout + H)
+        w, b = rnd(Cout, 3, 3, Cin, scale=(9 * Cin) ** -0.5, seed=Cout), rnd(Cout, scale=0.1, seed=Cout + 1)
+        out = []
+        _with_tune([(21, narrow)], lambda: out.append(ops.conv3x3(x, nimg, H, H, ops.conv_weight(w), b)))
+        close(out[0], conv_ref(x, nimg, H, H, w, b))
 
 
 @pytest.mark.parametrize("Cin,Cout,Cin2,nimg,res", [(320, 320, 0, 16, True), (960, 320, 0, 2, False), (640, 320, 0, 3, False),
