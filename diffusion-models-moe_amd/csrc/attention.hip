@@ -68,7 +68,7 @@ SDMOE_DEV void bld16(__amdgpu_buffer_rsrc_t rs, const half_t* lds_dst, unsigned 
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)lds_dst, 16, voff, 0, 0, 0);
 }
 
-template <int D, int NQF, int NW = 4, int POLY = 0, int ONESK = 0>
+template <int D, int NQF, int NW = 4, int POLY = 0>
 __global__ __launch_bounds__(NW * 64, (D >= 160 || NW >= 8 ? 1 : 2)) void attn_fwd_kernel(AttnParams p) {
   constexpr int DK = ((D + 31) / 32) * 32;   // contraction dim padded for 16x16x32
   constexpr int DV = ((D + 15) / 16) * 16;   // output dim padded to 16-row fragments
@@ -87,12 +87,6 @@ __global__ __launch_bounds__(NW * 64, (D >= 160 || NW >= 8 ? 1 : 2)) void attn_f
   constexpr int KBUF = TILE + 64;             // + zeroed tail for the over-read of the last K row
   constexpr bool SUM_BY_MFMA = DV > D;        // O^T row D accumulates sum_k P[k][q] (V column D := 1.0)
   static_assert(!SUM_BY_MFMA || D % 16 == 8, "ones column sits at the start of a 4-column tr-read group");
-  // ONESK: -m through a spare contraction column instead of the score accumulator's initial value: K[:, D] := 1 (one
-  // ds_write per lane and tile, by every wave -- each reads only its own write, so no barrier) and Q~[:, D] := -m in
-  // fp16 (lanes g = (D % 32) / 8 of chunk D / 32, element D % 8), so the score MFMAs start from 0 (inline constant)
-  // and the 8 accumulator moves per tile go. m is kept fp16-representable: the shift actually in Q~ is the one the
-  // softmax uses, so numerator and denominator see the same factor.
-  static_assert(!ONESK || (D < DK && D < RS && D % 8 == 0), "needs a spare K column inside the row and the contraction");
   constexpr float RESCALE_THR = 8.0f;
   constexpr unsigned OOB = 0x80000000u;
 
@@ -196,14 +190,13 @@ __global__ __launch_bounds__(NW * 64, (D >= 160 || NW >= 8 ? 1 : 2)) void attn_f
     const half_t* Vt = Kt + KBUF;
     // the other slot was last read in tile kt-1, which every wave finished before the previous barrier
     if (kt + 1 < nkt) issue_tile(BUF ? S0 : S1);
-    if constexpr (ONESK) const_cast<half_t*>(Kt)[lane * RS + D] = (half_t)1.f;  // K[key][D] = 1 for this tile
 
     // ---- S'^T = K Q~^T - m: the accumulator starts at -m (running max, log2 units), so after the MFMAs it
     //      holds exp2's argument directly (tile 0 starts at 0 and sets m from its own max)
     float4v s[NQF][4];
 #pragma unroll
     for (int f = 0; f < NQF; ++f) {
-      const float nm = ONESK ? 0.f : -mrun[f];
+      const float nm = -mrun[f];
 #pragma unroll
       for (int kf = 0; kf < 4; ++kf) s[f][kf] = (float4v){nm, nm, nm, nm};
     }
@@ -239,23 +232,14 @@ __global__ __launch_bounds__(NW * 64, (D >= 160 || NW >= 8 ? 1 : 2)) void attn_f
       // lane-local max: the wave-uniform rescale test needs no cross-lane step (all lane maxima <= THR iff all row
       // maxima are); the row max over the 4 lanes of a query (l, l^16, l^32, l^48) only where m moves
       const float ml = max2(m0, m2);
-      auto set_shift = [&](float m) {  // ONESK: -m into Q~'s spare column (lanes of column group D % 32 / 8)
-        if constexpr (ONESK) {
-          if (g == (D % 32) / 8) qf[f][D / 32][D % 8] = (half_t)(-m);
-        }
-      };
       if (kt == 0) {  // first tile: m = its max (O and l are still zero)
-        const float mx0 = max_xrows(ml);
-        const float mx = ONESK ? (float)(half_t)mx0 : mx0;
+        const float mx = max_xrows(ml);
         mrun[f] = mx;
-        set_shift(mx);
 #pragma unroll
         for (int kf = 0; kf < 4; ++kf) s[f][kf] -= mx;
       } else if (!__all(ml <= RESCALE_THR)) {  // wave-uniform decision
-        const float d0 = fmaxf(max_xrows(ml), 0.f);
-        const float delta = ONESK ? (float)(half_t)(mrun[f] + d0) - mrun[f] : d0;  // exact: both shifts in use
+        const float delta = fmaxf(max_xrows(ml), 0.f);
         mrun[f] += delta;
-        set_shift(mrun[f]);
         const float alpha = __builtin_amdgcn_exp2f(-delta);
         if (!SUM_BY_MFMA) lrun[f] *= alpha;
 #pragma unroll
@@ -659,9 +643,6 @@ int launch(const AttnParams& p, int nimg, hipStream_t s) {
   } else if (use8 && D <= 80) {
     dim3 grid((p.Nq + 255) / 256, p.heads, nimg);
     attn_fwd_kernel<D, 2, (D <= 80 ? 8 : 4)><<<grid, (D <= 80 ? 512 : 256), 0, s>>>(p);
-  } else if (g_attn_nqf == 41 && D == 40) {
-    dim3 grid((p.Nq + 255) / 256, p.heads, nimg);
-    attn_fwd_kernel<D, 2, 8, 0, (D == 40 ? 1 : 0)><<<grid, 512, 0, s>>>(p);
   } else if (g_attn_nqf == 40 && D == 40) {
     dim3 grid((p.Nq + 255) / 256, p.heads, nimg);
     attn_fwd_kernel<D, 2, 8, (D == 40 ? 1 : 0)><<<grid, 512, 0, s>>>(p);
@@ -679,7 +660,7 @@ int launch(const AttnParams& p, int nimg, hipStream_t s) {
 }  // namespace
 
 int sdmoe_attn_set_nqf(int v) {
-  if (v != 0 && v != 1 && v != 2 && v != 4 && v != 8 && v != 16 && v != 40 && v != 41) return SDMOE_EARG;
+  if (v != 0 && v != 1 && v != 2 && v != 4 && v != 8 && v != 16 && v != 40) return SDMOE_EARG;
   g_attn_nqf = v;
   return SDMOE_OK;
 }
