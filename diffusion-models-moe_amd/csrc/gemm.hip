@@ -1284,7 +1284,8 @@ int try_halo(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
 // [v 2 | g 2] layout: 150.9-154.3 vs 178.2-186.2 us at M = 16384, C = 640; SDXL pipeline +4.0 %, same box);
 // 0 = 256x160 4x2 tiles (rounds 3-4 until the layout change: 364 B/lane of scratch on 256x320)
 int g_gt320 = 1;
-X
+int g_narrow = 1;  // knob 21: 1 (default) = N <= 32 conv outputs (conv_out's 8 padded channels) on 128x32 tiles
+                   // (31.9 vs 34.8-35.1 us at 64x64 x 320 -> 8, same box), 0 = 128x64
 
 // routed-GEGLU linear: BN in {160, 320} tiles only (wave tile width 80 = 40 neurons = whole experts), no split-K
 template <int MODE>

@@ -365,7 +365,8 @@ int sdmoe_cfg_multistep_step(const void* eps, long lde, float* lat, int B, int H
    2 = every 128-row halo tile instead, 3 = the default plus 32-wide outputs on 256-row tiles, 0 = off;
    knob 17 = sdmoe_groupnorm above 256 positions: 0 (default) statistics kernels + apply, 1 = wide slice sums +
    one finalize-and-apply launch;
-   knob 20 = table-GELU routed GEGLU tiles: 1 (default) 256x320 like the ReLU kernel, 0 = 256x160 (4x2 waves). */
+   knob 20 = table-GELU routed GEGLU tiles: 1 (default) 256x320 like the ReLU kernel, 0 = 256x160 (4x2 waves);
+   knob 21 = convs with at most 32 output channels (conv_out): 1 (default) 128x32 tiles, 0 = 128x64. */
 int sdmoe_tune(int knob, int value);
 
 /*

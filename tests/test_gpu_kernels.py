@@ -370,7 +370,7 @@ def _with_tune(settings, fn):
         _lib.check(lib.sdmoe_tune(1, 0), "tune")
         _lib.check(lib.sdmoe_tune(16, 1), "tune")
         _lib.check(lib.sdmoe_tune(20, 1), "tune")
-        _lib.check(lib.sdmoe_tune(21, 0), "tune")
+        _lib.check(lib.sdmoe_tune(21, 1), "tune")
 
 
 # tiles (sdmoe_tune knob 1): 0 auto, 1 = 128x160, 2 = 64x160, 3 = 256x320 (2x4 waves), 4 = 256x160 (4x2), 5 = 256x320

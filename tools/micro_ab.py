@@ -18,7 +18,7 @@ DEV = "cuda"
 N_IMG = 16
 
 
-DEFAULTS = {"7": 1, "8": 1, "14": 1, "16": 1, "20": 1}  # sdmoe_tune knobs whose default is not 0
+DEFAULTS = {"7": 1, "8": 1, "14": 1, "16": 1, "20": 1, "21": 1}  # sdmoe_tune knobs whose default is not 0
 
 
 def rnd(*shape, scale=1.0):
