@@ -25,6 +25,12 @@ def key_flops(name, a, k, out):
         Cout, stride, up = a[15], a[16], a[17]
         M = out.shape[0]
         return (f"conv {H}x{W} s{stride}{'u' if up else ''} {Cin}->{Cout} M={M}", 2.0 * M * Cout * 9 * Cin, 0)
+    if name == "conv3x3_gn_launch":  # same leading arguments; GroupNorm(+SiLU) applied inside the halo conv
+        if out is None:  # shape not normalised in the kernel: the caller falls back (apply + conv, timed there)
+            return ("conv+gn declined", 0, 0)
+        nimg, H, W, Cin, Cout = a[2], a[3], a[4], a[5], a[15]
+        M = out.shape[0]
+        return (f"conv+gn {H}x{W} s1 {Cin}->{Cout} M={M}", 2.0 * M * Cout * 9 * Cin, 0)
     if name == "linear":
         x, w = a[0], a[1]
         M, K = x.shape
@@ -99,7 +105,7 @@ def main():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--evals", type=int, default=2)
     a = ap.parse_args()
-    for n in ("conv3x3_launch", "linear", "linear_ln", "linear_geglu", "linear_keep", "groupnorm", "attention", "groupnorm_stats", "groupnorm_apply",
+    for n in ("conv3x3_launch", "conv3x3_gn_launch", "linear", "linear_ln", "linear_geglu", "linear_keep", "groupnorm", "attention", "groupnorm_stats", "groupnorm_apply",
               "layernorm", "moe_topk_mask", "moe_topk_keep", "add", "mask_weight", "geglu_route", "gn_fold",
               "linear_per_image"):
         wrap(n)
