@@ -59,9 +59,6 @@ def parse():
     p.add_argument("--e2e-steps", type=int, default=1,
                    help="after the timed metric run, time this many end-to-end steps (text encoder + denoise + VAE "
                         "decode to RGB) and report them as 'end_to_end' (0: skip)")
-    p.add_argument("--graphs", action="store_true",
-                   help="replay one captured HIP graph per denoising step (StableDiffusionPipeline.graphs; captured "
-                        "during the warm-up calls, which --warmup must therefore include: >= 1)")
     p.add_argument("--no-roofline", action="store_true")
     p.add_argument("--roofline-sample", type=int, default=25,
                    help="time the conv launches of every N-th U-Net evaluation (1 = every launch; event markers idle "
@@ -367,10 +364,6 @@ def main():
     _lib.load()
     U.FUSED_KEEP = args.topk_mask == "down"
     cfg, pipe, rec, wanda, set_e2e = build(args, world, rank, dev)
-    if args.graphs:
-        if args.warmup < 1:
-            raise SystemExit("bench.py --graphs: the step graphs are captured by the first call; use --warmup >= 1")
-        pipe.graphs = True
     # global prompt list: rank r takes its contiguous shard (per-prompt seeds use the global index)
     from sdmoe import distributed as D
     prompts = [f"synthetic prompt {i}" for i in range(world * args.batch)]

@@ -50,25 +50,12 @@ SDMOE_DEV float max_xrows(float v) {
   return max2(__uint_as_float(t[0]), __uint_as_float(t[1]));
 }
 
-// 2^x for x <= 8 (softmax arguments after the running-max shift): n = rint(x) by the 1.5 * 2^23 magic add, f = x - n
-// in [-0.5, 0.5], 2^f by a degree-3 near-minimax polynomial (max rel. error 2.2e-4, inside fp16's 2^-11 rounding of P), the
-// exponent added to the bit pattern; x below -126 clamps to 2^-126 (P then rounds to 0 in fp16 as v_exp's result does)
-SDMOE_DEV float exp2_poly(float x) {
-  x = fmaxf(x, -126.f);
-  const float t = x + 12582912.f;
-  const float f = x - (t - 12582912.f);
-  float q = __builtin_fmaf(f, 0.05286744f, 0.24215189f);
-  q = __builtin_fmaf(f, q, 0.69358675f);
-  q = __builtin_fmaf(f, q, 0.99996276f);
-  return __uint_as_float(__float_as_uint(q) + (__float_as_uint(t) << 23));
-}
-
 typedef __attribute__((address_space(3))) void lds_void_t;
 SDMOE_DEV void bld16(__amdgpu_buffer_rsrc_t rs, const half_t* lds_dst, unsigned voff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)lds_dst, 16, voff, 0, 0, 0);
 }
 
-template <int D, int NQF, int NW = 4, int POLY = 0>
+template <int D, int NQF, int NW = 4>
 __global__ __launch_bounds__(NW * 64, (D >= 160 || NW >= 8 ? 1 : 2)) void attn_fwd_kernel(AttnParams p) {
   constexpr int DK = ((D + 31) / 32) * 32;   // contraction dim padded for 16x16x32
   constexpr int DV = ((D + 15) / 16) * 16;   // output dim padded to 16-row fragments
@@ -252,12 +239,7 @@ __global__ __launch_bounds__(NW * 64, (D >= 160 || NW >= 8 ? 1 : 2)) void attn_f
       for (int kf = 0; kf < 4; ++kf)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          // POLY (evaluation variant, sdmoe_tune knob 4 = 40): the last 16-key column block's exp2 as a Cody-Waite
-          // reduction + degree-3 polynomial on the FMA pipe (8 plain VALU issues in place of one v_exp). Measured
-          // slower, so not the default: d = 40 N = 4096 515-521 vs 456-478 us, pipeline -2.1 % (same box). On gfx950
-          // v_exp_f32 issues in 8 cycles vs 4 for an FMA (MI355X_MICROARCH constants), so every polynomial exp costs
-          // ~4x the issue time of the transcendental it replaces in this issue-bound loop.
-          const float e = (POLY && !RAGGED && kf == 3) ? exp2_poly(s[f][kf][i]) : __builtin_amdgcn_exp2f(s[f][kf][i]);
+          const float e = __builtin_amdgcn_exp2f(s[f][kf][i]);
           s[f][kf][i] = e;
           if (!SUM_BY_MFMA) ls += e;
         }
@@ -613,8 +595,8 @@ __global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn32_kernel(AttnPar
 
 // sdmoe_tune knob 4: 0 = by shape (default): attn32_kernel for d = 80 self-attention (Nk > 128), the 16x16x32 kernel
 // in 8-wave workgroups for d = 40 / 64 self-attention (Nk > 128), the 4-wave 16x16x32 kernel (NQF = 2) everywhere
-// else; 1 = attn32_kernel; 2 or 4 = the 4-wave 16x16x32 kernel with NQF = 2 / 4; 8 / 16 = the 16x16x32 kernel in
-// 8-wave (d <= 80) / 16-wave (d <= 40) workgroups
+// else; 1 = attn32_kernel; 2 or 4 = the 4-wave 16x16x32 kernel with NQF = 2 / 4; 8 = the 16x16x32 kernel in
+// 8-wave workgroups (d <= 80)
 int g_attn_nqf = 0;
 
 template <int D>
@@ -643,12 +625,6 @@ int launch(const AttnParams& p, int nimg, hipStream_t s) {
   } else if (use8 && D <= 80) {
     dim3 grid((p.Nq + 255) / 256, p.heads, nimg);
     attn_fwd_kernel<D, 2, (D <= 80 ? 8 : 4)><<<grid, (D <= 80 ? 512 : 256), 0, s>>>(p);
-  } else if (g_attn_nqf == 40 && D == 40) {
-    dim3 grid((p.Nq + 255) / 256, p.heads, nimg);
-    attn_fwd_kernel<D, 2, 8, (D == 40 ? 1 : 0)><<<grid, 512, 0, s>>>(p);
-  } else if (g_attn_nqf == 16 && D <= 40) {
-    dim3 grid((p.Nq + 511) / 512, p.heads, nimg);
-    attn_fwd_kernel<D, 2, (D <= 40 ? 16 : 4)><<<grid, (D <= 40 ? 1024 : 256), 0, s>>>(p);
   } else {
     dim3 grid((p.Nq + 127) / 128, p.heads, nimg);
     attn_fwd_kernel<D, 2><<<grid, 256, 0, s>>>(p);
@@ -660,7 +636,7 @@ int launch(const AttnParams& p, int nimg, hipStream_t s) {
 }  // namespace
 
 int sdmoe_attn_set_nqf(int v) {
-  if (v != 0 && v != 1 && v != 2 && v != 4 && v != 8 && v != 16 && v != 40) return SDMOE_EARG;
+  if (v != 0 && v != 1 && v != 2 && v != 4 && v != 8) return SDMOE_EARG;
   g_attn_nqf = v;
   return SDMOE_OK;
 }

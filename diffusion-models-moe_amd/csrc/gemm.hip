@@ -25,17 +25,10 @@ namespace {
 
 constexpr int BK = 64;
 
-// 1: software-pipelined MFMA fragment reads in the GEMM main loop (next A pair read before the current pair's MFMAs);
-// 0: all fragments of a 32-deep slice read, then its MFMAs (kept buildable for same-box A/B: make GEMM_PIPE=0)
-#ifndef SDMOE_GEMM_PIPE
-#define SDMOE_GEMM_PIPE 1
-#endif
-
 // tuning knobs (sdmoe_tune): 0 = LDS stages (0 = auto, 2 or 3); 1 = forced tile config (0 = auto)
 int g_stages = 0;
 int g_tile = 0;
 int g_bk = 0;
-int g_prio = 0;
 int g_res16 = 1;  // knob 8: 1 = residual epilogues on the fp16 staging path (residual added in the copy-out), 0 = fp32
 int g_ksplit = 0;  // knob 9: forced split-K factor (0 = auto; 1 = never split), for tile sweeps
 int g_mfast = 1;   // knob 14: split-K conv grids ordered M-tile fastest (1) or split fastest (0)
@@ -67,7 +60,6 @@ struct GemmParams {
   // contiguous esize-neuron experts (neurons pre-permuted so every expert is contiguous)
   half_t* score; long ld_score;
   int esize;
-  int prio;  // experiment knob: raise wave priority around the MFMA block
   int res16;  // residual on the fp16 staging path (sdmoe_tune knob 8)
   int diag;  // diagnostic knob (sdmoe_tune 6): bit 0 skips the K-loop loads, bit 1 the MFMAs
   // expert keep mask of the A operand (MODE_KEEP / MODE_KEEPW): keep[(k / 64) * M * 8 + m * 8 + (k % 64) / 8] bit
@@ -730,7 +722,6 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
 
     const char* sa = smem + (it % NSTAGE) * STAGE;
     const char* sbm = sa + BM * BK * 2;
-    if (p.prio) __builtin_amdgcn_s_setprio(1);
     if (p.diag & 2) continue;
     // fragment reads (A masked by MoE keep bits, B by Wanda bits where the mode says so)
     auto read_a = [&](int kk, int i) -> half8 {
@@ -759,7 +750,7 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
       }
       return b;
     };
-    if constexpr (SDMOE_GEMM_PIPE && !(KEEP && FN > 5)) {  // (wide masked tiles: no registers to spare)
+    if constexpr (!(KEEP && FN > 5)) {  // (wide masked tiles: no registers to spare)
       // software-pipelined: A fragments in pairs, the next pair's LDS reads issued before the current pair's
       // 2*FN MFMAs (one group of latency cover); the next kk's B fragments read during the last group when they
       // fit a second register set. sched_barrier pins the read / MFMA order so hipcc cannot sink the reads to
@@ -834,7 +825,6 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
         }
       }
     }
-    if (p.prio) __builtin_amdgcn_s_setprio(0);
   }
   }  // !HALO
 
@@ -1178,7 +1168,6 @@ int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s, int ks_w
   // every XCD (PMC FETCH_SIZE of the split-K conv launches 140 -> 46 MB, time neutral); the M = 1024 split-K linears
   // measured 2 us slower with it
   p.mfast = (p.ksplit > 1 && g_mfast && (MODE == MODE_CONV || MODE == MODE_CONV_UP)) ? 1 : 0;
-  p.prio = g_prio;
   p.diag = g_diag;
   p.res16 = g_res16;
   const dim3 grid(ntiles * p.ksplit);
@@ -1238,7 +1227,6 @@ int launch_halo(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
   p.kchunk2 = p.A2 ? ((p.K - 9 * p.Cin) / 32 + p.ksplit - 1) / p.ksplit : 0;  // shortcut steps per split
   p.part = p.ksplit > 1 ? ws : nullptr;
   p.mfast = p.ksplit > 1 ? g_mfast : 0;
-  p.prio = g_prio;
   p.diag = g_diag;
   p.res16 = g_res16;
   (void)HW_;
@@ -1805,19 +1793,16 @@ extern "C" int sdmoe_mask_weight(const void* W, const void* bits, long N, long K
 
 int sdmoe_attn_set_nqf(int v);  // attention.hip
 int sdmoe_gn_set_fused(int v);  // norm.hip
-int sdmoe_gn_set_split(int v);  // norm.hip
 extern int g_topk_tpw;          // moe.hip
 
 extern "C" int sdmoe_tune(int knob, int value) {
   if (knob == 4) return sdmoe_attn_set_nqf(value);
   if (knob == 7) return sdmoe_gn_set_fused(value);
-  if (knob == 17) return sdmoe_gn_set_split(value);
   if (knob == 0 && (value == 0 || value == 2 || value == 3)) { g_stages = value; return SDMOE_OK; }
   if (knob == 1 && value >= 0 && value <= 8) { g_tile = value; return SDMOE_OK; }
   if (knob == 9 && value >= 0 && value <= 16) { g_ksplit = value; return SDMOE_OK; }
   if (knob == 14 && (value == 0 || value == 1)) { g_mfast = value; return SDMOE_OK; }
   if (knob == 2 && (value == 0 || value == 32 || value == 64)) { g_bk = value; return SDMOE_OK; }
-  if (knob == 3 && (value == 0 || value == 1)) { g_prio = value; return SDMOE_OK; }
   if (knob == 6 && value >= 0 && value <= 63) { g_diag = value; return SDMOE_OK; }
   if (knob == 8 && (value == 0 || value == 1)) { g_res16 = value; return SDMOE_OK; }
   if (knob == 15 && (value == 0 || value == 1 || value == 4)) { g_topk_tpw = value; return SDMOE_OK; }

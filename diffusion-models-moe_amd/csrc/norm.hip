@@ -18,8 +18,6 @@ int g_gn_fused = 1;  // sdmoe_tune knob 7, sdmoe_groupnorm at HW <= GN_FUSED_HW:
 // at 16x16; at 32x32 it is slower (21.9 vs 21.1 us, C = 640; 47.6 vs 42.2 at C = 1920): every block re-reads its
 // chunk's 1024 rows with 16 KB in flight, which no longer hides behind the saved launch (tools/micro_ab.py gn)
 constexpr int GN_FUSED_HW = 256;
-int g_gn_split = 0;  // sdmoe_tune knob 17, sdmoe_groupnorm above GN_FUSED_HW: 1 = partial sums + finalize-and-apply
-                     // (two wide launches), 0 = statistics kernel(s) + gn_apply_kernel
 
 // chunk width of the small-latent kernels: whole groups and whole 16-B chunks (lcm(cpg, 8)), doubled towards 80
 // channels while the chunk count stays integral; 0 when no such chunk exists
@@ -398,80 +396,6 @@ __global__ __launch_bounds__(64) void gn_finalize_kernel(const half_t* __restric
   }
 }
 
-// Finalize + apply(+SiLU) in one launch (after gn_partial_kernel): block (row chunk, image) first combines its
-// image's S slice sums of every group (8 threads per group, fp64, as gn_finalize_kernel) into per-channel fp32
-// scale / shift in LDS -- chunk 0 also stores them -- then applies them to its RB rows. Replaces gn_small_kernel (one
-// block per 80-channel chunk: 128 blocks at 32x32 x 640, latency-bound at ~13 us) or gn_finalize_kernel, plus
-// gn_apply_kernel: two launches, both wide.
-constexpr int GN_APPLY_RB = 32;  // rows per apply block
-__global__ __launch_bounds__(256) void gn_apply_fin_kernel(const half_t* __restrict__ X, long ldx, int HW, int C,
-                                                           int G, int S, const float2* __restrict__ part,
-                                                           const half_t* __restrict__ gamma,
-                                                           const half_t* __restrict__ beta, float eps, int silu,
-                                                           half_t* __restrict__ Y, long ldy,
-                                                           float* __restrict__ scale, float* __restrict__ shift) {
-  __shared__ float4v sc_l[2560 / 4], sh_l[2560 / 4];
-  __shared__ float stat[64][2];
-  const int chunk = blockIdx.x, img = blockIdx.y, tid = threadIdx.x;
-  const int cpg = C / G;
-  {
-    const int g = tid >> 3, j = tid & 7;  // 32 groups per pass of 8 threads each
-    for (int g0 = 0; g0 < G; g0 += 32) {
-      const int gg = g0 + g;
-      double a = 0.0, b = 0.0;
-      if (gg < G)
-        for (int s = j; s < S; s += 8) {
-          const float2 v = part[((long)img * G + gg) * S + s];
-          a += v.x;
-          b += v.y;
-        }
-#pragma unroll
-      for (int o = 4; o > 0; o >>= 1) { a += __shfl_xor(a, o, 64); b += __shfl_xor(b, o, 64); }
-      if (j == 0 && gg < G) {
-        const double n = (double)HW * cpg;
-        const double ref = (double)(float)X[(long)img * HW * ldx + gg * cpg];
-        const double m1 = a / n;
-        double var = b / n - m1 * m1;
-        if (var < 0) var = 0;
-        stat[gg][0] = (float)(ref + m1);
-        stat[gg][1] = (float)(1.0 / sqrt(var + (double)eps));
-      }
-    }
-  }
-  __syncthreads();
-  float* scf = reinterpret_cast<float*>(sc_l);
-  float* shf = reinterpret_cast<float*>(sh_l);
-  for (int c = tid; c < C; c += 256) {
-    const int g = c / cpg;
-    const float sc = stat[g][1] * (float)gamma[c];
-    const float sh = (float)beta[c] - stat[g][0] * sc;
-    scf[c] = sc;
-    shf[c] = sh;
-    if (chunk == 0) {
-      scale[(long)img * C + c] = sc;
-      shift[(long)img * C + c] = sh;
-    }
-  }
-  __syncthreads();
-  const int cpr = C / 8;
-  const int r0 = chunk * GN_APPLY_RB, nr = min(GN_APPLY_RB, HW - r0);
-  const long rowbase = (long)img * HW + r0;
-  for (int id = tid; id < nr * cpr; id += 256) {
-    const int r = id / cpr, c = (id - r * cpr) * 8;
-    const half8 x = *reinterpret_cast<const half8*>(X + (rowbase + r) * ldx + c);
-    const float4v s0 = sc_l[c / 4], s1 = sc_l[c / 4 + 1], h0 = sh_l[c / 4], h1 = sh_l[c / 4 + 1];
-    const float sv[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
-    const float hv[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
-    half8 o;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float f = (float)x[j] * sv[j] + hv[j];
-      if (silu) f = silu_f(f);
-      o[j] = (half_t)f;
-    }
-    *reinterpret_cast<half8*>(Y + (rowbase + r) * ldy + c) = o;
-  }
-}
 
 // LayerNorm over the last dim (C % 64 == 0, C <= 2048): 8 lanes per row, 8 rows per wave, blockDim/8 rows per
 // block (4 waves; 1 wave when M is small, so the 16x16 / 8x8 latents' few thousand rows still cover every CU);
@@ -557,12 +481,6 @@ int groupnorm_impl(const void* X, long ldx, int nimg, int HW, int C, int groups,
 }
 }  // namespace
 
-int sdmoe_gn_set_split(int v) {
-  if (v < 0 || v > 1) return SDMOE_EARG;
-  g_gn_split = v;
-  return SDMOE_OK;
-}
-
 int sdmoe_gn_set_fused(int v) {
   if (v < 0 || v > 2) return SDMOE_EARG;
   g_gn_fused = v;
@@ -603,28 +521,6 @@ extern "C" int sdmoe_groupnorm(const void* X, long ldx, int nimg, int HW, int C,
         gn_fused_kernel<<<grid, 256, 0, st>>>(x, ldx, HW, C, groups, wc, S, g, b, eps, silu, (half_t*)Y, ldy, scale,
                                               shift);
       }
-      SDMOE_CHECK_LAUNCH();
-      return SDMOE_OK;
-    }
-  }
-  // wide partial sums, then finalize + apply in one launch (32x32 latents, conv_norm_out)
-  if (g_gn_split && HW > GN_FUSED_HW && X && gamma && beta && nimg > 0 && groups > 0 && groups <= 64 && C % groups == 0 && C % 8 == 0 &&
-      C <= 2560 && ldx % 8 == 0 && workspace && HW >= 64) {
-    int S = (1024 + nimg - 1) / nimg;
-    if (S > HW / 32) S = HW / 32;  // slices of >= 32 rows: the apply blocks combine S sums per group
-    if (S > 64) S = 64;
-    if (S < 1) S = 1;
-    if ((long)nimg * groups * S * 2 <= workspace_floats) {
-      hipStream_t s = (hipStream_t)stream;
-      float2* part = reinterpret_cast<float2*>(workspace);
-      if (C / 8 > 256)
-        gn_partial_kernel<2><<<dim3(S, nimg), 256, 0, s>>>((const half_t*)X, ldx, HW, C, groups, S, part);
-      else
-        gn_partial_kernel<1><<<dim3(S, nimg), 256, 0, s>>>((const half_t*)X, ldx, HW, C, groups, S, part);
-      SDMOE_CHECK_LAUNCH();
-      gn_apply_fin_kernel<<<dim3((HW + GN_APPLY_RB - 1) / GN_APPLY_RB, nimg), 256, 0, s>>>(
-          (const half_t*)X, ldx, HW, C, groups, S, part, (const half_t*)gamma, (const half_t*)beta, eps, silu,
-          (half_t*)Y, ldy, scale, shift);
       SDMOE_CHECK_LAUNCH();
       return SDMOE_OK;
     }

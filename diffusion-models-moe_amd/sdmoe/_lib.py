@@ -84,7 +84,9 @@ def load(path: str | None = None):
             "(or `make -C diffusion-models-moe_amd/csrc`). There is no CPU fallback."
         )
     lib = ctypes.CDLL(p)
-    ab_lib = "SDMOE_LIB" in os.environ  # same-box A/B against an older build: entry points it lacks stay unbound
+    # same-box A/B against an older build (SDMOE_AB=1, with SDMOE_LIB naming it): entry points it lacks stay unbound
+    # and the callers that probe with has() take their older path; otherwise a missing symbol is an error
+    ab_lib = os.environ.get("SDMOE_AB", "0") == "1"
     for name, argt in SIGNATURES.items():
         if ab_lib and not hasattr(lib, name):
             continue
@@ -92,11 +94,29 @@ def load(path: str | None = None):
         fn.argtypes = argt
         fn.restype = ctypes.c_char_p if name == "sdmoe_version" else ctypes.c_int
     # A/B experiments without code changes: SDMOE_TUNE="knob=value,..." (sdmoe_tune, include/sdmoe.h)
-    for kv in filter(None, os.environ.get("SDMOE_TUNE", "").split(",")):
-        k, v = kv.split("=")
-        check(lib.sdmoe_tune(int(k), int(v)), f"sdmoe_tune({kv})")
+    for k, v in parse_tune(os.environ.get("SDMOE_TUNE", "")):
+        check(lib.sdmoe_tune(k, v), f"sdmoe_tune({k}={v})")
     _lib = lib
     return lib
+
+
+def parse_tune(spec: str):
+    """SDMOE_TUNE="knob=value,..." -> [(knob, value)]; malformed entries raise SdmoeError (not a bare ValueError)."""
+    out = []
+    for kv in filter(None, (s.strip() for s in spec.split(","))):
+        parts = kv.split("=")
+        if len(parts) != 2:
+            raise SdmoeError(f"SDMOE_TUNE entry {kv!r}: expected knob=value")
+        try:
+            out.append((int(parts[0]), int(parts[1])))
+        except ValueError:
+            raise SdmoeError(f"SDMOE_TUNE entry {kv!r}: knob and value must be integers") from None
+    return out
+
+
+def has(lib, name: str) -> bool:
+    """Whether the loaded library exports `name` (only an SDMOE_AB=1 build may lack one)."""
+    return hasattr(lib, name)
 
 
 def check(status: int, what: str):

@@ -262,7 +262,8 @@ FUSED_GN = os.environ.get("SDMOE_FUSED_GN", "1") != "0"  # GroupNorm(+SiLU) insi
 
 def conv_gn_fusable(H, W, Cin, Cout):
     """Shapes whose conv applies a GroupNorm in the kernel (sdmoe_conv3x3_gn: the 64-wide halo tiles)."""
-    return FUSED_GN and W == 64 and (H * W) % 256 == 0 and Cin <= 1280 and Cin % 64 == 0 and Cout % 320 == 0
+    return (FUSED_GN and W == 64 and (H * W) % 256 == 0 and Cin <= 1280 and Cin % 64 == 0 and Cout % 320 == 0
+            and _lib.has(_lib.load(), "sdmoe_conv3x3_gn"))
 
 
 def _conv3x3_gn(lib, x, nimg, H, W, w, bias, out, residual, coladd, coladd_bstride, gn, shortcut):
@@ -550,10 +551,11 @@ def ensure_gelu_table(device) -> torch.Tensor:
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     t = _GELU_TABLES.get(idx)
     if t is None:
-        vals = torch.nn.functional.gelu(gelu_table_values())  # fp16 CPU, as the reference's fp16 gate
-        t = vals.to(torch.device("cuda", idx)).contiguous()
+        # F.gelu on the DEVICE fp16 tensor: the reference hook applies module.gelu to the gate on the GPU the model
+        # sits on (base_receiver.py model.to(args.gpu); moefy.py:13, remove_skilled_experts.py:27)
+        t = torch.nn.functional.gelu(gelu_table_values().to(torch.device("cuda", idx))).contiguous()
         lib = _lib.load()
-        if hasattr(lib, "sdmoe_set_gelu_table"):  # (an older A/B build evaluates GELU itself)
+        if _lib.has(lib, "sdmoe_set_gelu_table"):  # (an older A/B build evaluates GELU itself)
             with torch.cuda.device(idx):
                 _lib.check(lib.sdmoe_set_gelu_table(t.data_ptr()), "sdmoe_set_gelu_table")
         _GELU_TABLES[idx] = t

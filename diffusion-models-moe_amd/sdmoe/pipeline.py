@@ -120,56 +120,6 @@ class PipelineOutput:
     images: list
 
 
-def hook_owners(unet):
-    """The receivers whose forward hooks sit on the U-Net, in module order, or None when a hook is not a sdmoe
-    receiver method without host-side gate capture (graph replay would skip its Python side effects). A step graph
-    replays the kernels those hooks launched; what it cannot replay is their host state, which for these receivers
-    is exactly the (timestep, layer) counter (predictivity.py:25-39) -- emulated per step by StepGraphs."""
-    owners = []
-    for m in unet.modules():
-        for fn in getattr(m, "_forward_hooks", {}).values():
-            o = getattr(fn, "__self__", None)
-            if o is None or not getattr(o, "_sdmoe_receiver", False) or getattr(o, "store_gates", True):
-                return None
-            if all(o is not q for q in owners):
-                owners.append(o)
-    return owners
-
-
-def _counter(o):
-    return (getattr(o, "timestep", None), getattr(o, "layer", None))
-
-
-def _set_counter(o, c):
-    if c[0] is not None:
-        o.timestep, o.layer = c
-
-
-class StepGraphs:
-    """One captured HIP graph per denoising step of a pipeline call (U-Net evaluation + CFG/scheduler update) over
-    static input/output buffers, replayed in order by later calls with the same signature. Launch-bound regimes
-    (one prompt per call, base_receiver.py:73: ~430 kernels per U-Net evaluation of a few us each) stop paying the
-    host's per-op Python + launch cost. counters[s] = (before, after) counter values of every hook owner around
-    step s's capture: a replay checks `before` and sets `after`, so the receivers' (t, l) state is exactly what
-    the eager hooks would leave."""
-
-    def __init__(self, owners):
-        self.owners = owners
-        self.graphs = []
-        self.counters = []
-        self.bufs = {}
-
-    def replay(self):
-        for g, (pre, post) in zip(self.graphs, self.counters):
-            for o, c in zip(self.owners, pre):
-                if _counter(o) != c:
-                    raise RuntimeError(f"graph replay: {type(o).__name__} counter {_counter(o)} != captured {c}; "
-                                       f"reset the receiver (reset_time_layer) or call pipe.reset_graphs()")
-            g.replay()
-            for o, c in zip(self.owners, post):
-                _set_counter(o, c)
-
-
 class StableDiffusionPipeline:
     def __init__(self, unet: UNet2DConditionModel, device="cuda", num_inference_steps=50, guidance_scale=7.5,
                  scheduler="ddim", vae=None, text_encoder=None, tokenizer=None, text_encoder_2=None,
@@ -190,14 +140,6 @@ class StableDiffusionPipeline:
         self.tokenizer = tokenizer
         self.text_encoder_2 = text_encoder_2
         self.tokenizer_2 = tokenizer_2
-        # HIP-graph replay of the denoising steps (opt-in): the first call with a given signature runs eagerly and
-        # then captures one graph per step; later calls replay them. The caller promises that weights, routing and
-        # receiver masks stay fixed while graphs are kept (reset_graphs() after changing any of them).
-        self.graphs = False
-        self._graph_states = {}
-
-    def reset_graphs(self):
-        self._graph_states = {}
 
     @classmethod
     def synthetic(cls, cfg: UNetConfig | None = None, seed: int = 0, device="cuda", **kw):
@@ -276,29 +218,6 @@ class StableDiffusionPipeline:
                 add_hidden = add_hidden[B:]
         if not do_cfg:
             ctx = ctx[B * CTX_LEN:]
-        key, owners = None, None
-        if self.graphs:
-            owners = hook_owners(self.unet)
-            if owners is not None:
-                key = (B, steps, self.scheduler, float(g), tuple(ctx.shape),
-                       None if add_hidden is None else tuple(add_hidden.shape),
-                       tuple((id(o), type(o)) for o in owners),
-                       tuple((id(m), tuple(getattr(fn, "__func__", fn) for fn in m._forward_hooks.values()))
-                             for m in self.unet.modules() if getattr(m, "_forward_hooks", None)))
-        st = self._graph_states.get(key) if key is not None else None
-        if st is not None:  # replay the captured steps on this call's inputs
-            b = st.bufs
-            b["lat"].copy_(lat)
-            b["ctx"].copy_(ctx)
-            if add_hidden is not None:
-                b["add_hidden"].copy_(add_hidden)
-            if "hist" in b:
-                b["hist"].zero_()
-                b["cur"].zero_()
-            ops.prepare_input(b["lat"], b["x_in"], ncopy)
-            st.replay()
-            return PipelineOutput(images=self._finish(b["lat"].clone(), output_type or self.output_type))
-        before = [_counter(o) for o in owners] if key is not None else None
         HW = cfg.sample_size * cfg.sample_size
         x_in = torch.zeros((ncopy * B * HW, IN_PAD), dtype=torch.float16, device=self.device)
         eps = torch.empty((ncopy * B * HW, OUT_PAD), dtype=torch.float16, device=self.device)
@@ -306,33 +225,14 @@ class StableDiffusionPipeline:
         bufs = dict(lat=lat, x_in=x_in, eps=eps, ctx=ctx, add_hidden=add_hidden)
         self._denoise(bufs, steps, g, do_cfg)
         out = PipelineOutput(images=self._finish(lat, output_type or self.output_type))
-        if key is not None:  # capture this signature's step graphs for the next calls (receiver state restored)
-            after = [_counter(o) for o in owners]
-            for o, c in zip(owners, before):
-                _set_counter(o, c)
-            self._graph_states[key] = self._capture(bufs, owners, steps, g, do_cfg)
-            for o, c in zip(owners, after):
-                if _counter(o) != c:
-                    raise RuntimeError("graph capture left a receiver counter different from the eager run's")
         return out
 
-    def _denoise(self, bufs, steps, g, do_cfg, graphs=None):
-        """The denoising loop over bufs (lat, x_in, eps, ctx, add_hidden); with `graphs` (a StepGraphs) every step
-        is captured into its own graph instead of being run (the receivers' hooks still execute on the host)."""
+    def _denoise(self, bufs, steps, g, do_cfg):
+        """The denoising loop over bufs (lat, x_in, eps, ctx, add_hidden)."""
         lat, x_in, eps, ctx, add_hidden = (bufs[k] for k in ("lat", "x_in", "eps", "ctx", "add_hidden"))
 
         def temb_row(table, i):
             return None if table is None else table[i:i + 1]
-
-        def step(i, body):
-            if graphs is None:
-                return body()
-            pre = [_counter(o) for o in graphs.owners]
-            gr = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gr, pool=bufs["pool"]):
-                body()
-            graphs.graphs.append(gr)
-            graphs.counters.append((pre, [_counter(o) for o in graphs.owners]))
 
         time_table = self.unet.time_embed_table if PRECOMPUTE_TEMB else (lambda ts: None)
         if self.scheduler == "pndm":
@@ -346,7 +246,7 @@ class StableDiffusionPipeline:
                 def body(i=i, t=t, coef=coef, flags=flags):
                     self.unet.forward_nhwc(x_in, float(t), ctx, out=eps, add_hidden=add_hidden, temb=temb_row(table, i))
                     ops.cfg_multistep_step(eps, lat, do_cfg, g, hist, cur, coef, flags, next_in=x_in)
-                step(i, body)
+                body()
         else:
             ts, a_t, a_prev = ddim_schedule(steps)
             if "table" not in bufs:
@@ -356,19 +256,7 @@ class StableDiffusionPipeline:
                 def body(s=s, t=t):
                     self.unet.forward_nhwc(x_in, float(t), ctx, out=eps, add_hidden=add_hidden, temb=temb_row(table, s))
                     ops.cfg_ddim_step(eps, lat, do_cfg, g, a_t[s], a_prev[s], next_in=x_in)
-                step(s, body)
-
-    def _capture(self, bufs, owners, steps, g, do_cfg):
-        """Static copies of the call's buffers and one graph per step over them (StepGraphs)."""
-        st = StepGraphs(owners)
-        b = st.bufs
-        for k in ("lat", "x_in", "eps", "ctx", "add_hidden", "table"):
-            b[k] = None if bufs.get(k) is None else bufs[k].clone()
-        b["pool"] = torch.cuda.graph_pool_handle()
-        torch.cuda.synchronize()
-        self._denoise(b, steps, g, do_cfg, graphs=st)
-        torch.cuda.synchronize()
-        return st
+                body()
 
     def _finish(self, lat, output_type):
         """output_type "latent": the denoised latents; "pt" / "np": vae.decode(latents / scaling_factor) then

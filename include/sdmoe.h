@@ -69,8 +69,6 @@ int sdmoe_conv3x3_sc(const void* X, long ldx, int nimg, int H, int W, int Cin, c
                      const void* coladd, long coladd_bstride, const void* X2, long ldx2, int Cin2, void* Y, long ldy,
                      int Cout, int act, float* workspace, long workspace_floats, void* stream);
 
-/* Y = (SiLU?)(X * scale[img, c] + shift[img, c]) on [nimg*HW, C] (the GroupNorm apply; scale/shift from
- * sdmoe_groupnorm_stats). C % 8 == 0. */
 /*
  * Y = conv3x3(act(GroupNorm(X))) [+ X2 W_sc^T] (+ bias + coladd + R): the ResNet conv with the GroupNorm(+SiLU)
  * in front of it applied INSIDE the conv (diffusers ResnetBlock2D: conv1(silu(norm1(x))), conv2(silu(norm2(h)))):
@@ -85,6 +83,8 @@ int sdmoe_conv3x3_gn(const void* X, long ldx, int nimg, int H, int W, int Cin, c
                      const float* gn_shift, int silu, const void* Wt, const void* bias, const void* coladd,
                      long coladd_bstride, const void* R, long ldr, const void* X2, long ldx2, int Cin2, void* Y,
                      long ldy, int Cout, float* workspace, long workspace_floats, void* stream);
+/* Y = (SiLU?)(X * scale[img, c] + shift[img, c]) on [nimg*HW, C] (the GroupNorm apply; scale/shift from
+ * sdmoe_groupnorm_stats). C % 8 == 0. */
 int sdmoe_groupnorm_apply(const void* X, long ldx, int nimg, int HW, int C, const float* scale, const float* shift,
                           int silu, void* Y, long ldy, void* stream);
 
@@ -349,11 +349,9 @@ int sdmoe_cfg_multistep_step(const void* eps, long lde, float* lat, int B, int H
    7 = 128x160 8-wave, 8 = 64x320 8-wave; 7/8 plain GEMM / conv / LN-folded GEMM only); knob 9 = forced split-K
    factor (0 auto, 1 = never split, 2..16); knob 14 = split-K conv tile order: 1 (default) M-tile fastest (one XCD's
    workgroups share weight slices in its L2), 0 split fastest; knob 2 = K-step
-   depth (0 auto, 32, 64); knob 3 = MFMA-cluster wave priority (0/1); knob 4 = attention kernel (0 auto by shape,
+   depth (0 auto, 32, 64); knob 4 = attention kernel (0 auto by shape,
    1 = 32x32x16 MFMA kernel, 2 / 4 = 4-wave 16x16x32 kernel with 32 / 64 queries per wave, 64 for head_dim <= 40
-   only; 8 = 16x16x32 kernel in 8-wave workgroups (head_dim <= 80), 16 = in 16-wave workgroups (head_dim <= 40);
-   40 = the 8-wave kernel with a quarter of the exp2s as a polynomial on the FMA pipe (head_dim 40; evaluation only,
-   measured slower));
+   only; 8 = 16x16x32 kernel in 8-wave workgroups (head_dim <= 80));
    knob 6 = GEMM diagnostics bits (1 no K-loop loads, 2 no MFMA, 4 no epilogue, 8 no global stores);
    knob 7 = sdmoe_groupnorm at HW <= 256: 1 (default) statistics + apply in one launch with the rows held in
    registers, 2 the same launch re-reading the rows for the apply, 0 two launches;
@@ -363,8 +361,6 @@ int sdmoe_cfg_multistep_step(const void* eps, long lde, float* lat, int B, int H
    bits at E <= 64 with one quad of lanes per token; 1 / 4 = always the ballot kernel at one / four tokens per wave;
    knob 16 = halo-tiled 3x3 convs: 1 (default) where measured faster (64- and 16-wide outputs, the upsample convs),
    2 = every 128-row halo tile instead, 3 = the default plus 32-wide outputs on 256-row tiles, 0 = off;
-   knob 17 = sdmoe_groupnorm above 256 positions: 0 (default) statistics kernels + apply, 1 = wide slice sums +
-   one finalize-and-apply launch;
    knob 20 = table-GELU routed GEGLU tiles: 1 (default) 256x320 like the ReLU kernel, 0 = 256x160 (4x2 waves);
    knob 21 = convs with at most 32 output channels (conv_out): 1 (default) 128x32 tiles, 0 = 128x64. */
 int sdmoe_tune(int knob, int value);

@@ -663,38 +663,21 @@ def test_groupnorm_single_launch_bit_identical(HW, C, nimg, silu):
     close(outs[0][:, 8:8 + C], F.silu(ref) if silu else ref, tol=5e-3)
 
 
-GN_SPLIT_DEFAULT = 0  # norm.hip g_gn_split
-
-
 @pytest.mark.parametrize("HW,C,nimg,silu", [(1024, 640, 16, True), (1024, 1920, 16, True), (1024, 2560, 3, False),
                                             (4096, 320, 16, True), (300, 960, 5, True), (2048, 640, 1, False),
                                             (1024, 1280, 2, True)])
-def test_groupnorm_partial_then_finalize_apply(HW, C, nimg, silu):
-    """sdmoe_groupnorm above 256 positions (sdmoe_tune knob 17 = 1): wide slice sums + one finalize-and-apply
-    launch (gn_apply_fin_kernel) vs the statistics kernels + gn_apply_kernel (knob 17 = 0) and vs torch fp32; the
-    scale / shift outputs too; strided output view, row tails (HW % 32 != 0), C > 2048 (two virtual threads)."""
-    from sdmoe import _lib
-    lib = _lib.load()
+def test_groupnorm_large_latents(HW, C, nimg, silu):
+    """sdmoe_groupnorm above 256 positions (statistics kernels + gn_apply_kernel) vs torch fp32, into a strided output
+    view whose neighbouring columns must stay untouched; row tails (HW % 32 != 0) and C > 2048."""
     buf = rnd(nimg * HW, C + 64, seed=HW + C + 5) * 2 + 1
     x = buf[:, 64:]
     gamma, beta = rnd(C, scale=0.1, seed=C + 3) + 1, rnd(C, scale=0.1, seed=C + 4)
-    outs = []
-    for mode in (1, 0):
-        _lib.check(lib.sdmoe_tune(17, mode), "tune")
-        try:
-            dst = torch.full((nimg * HW, C + 16), 7.0, dtype=torch.float16, device=DEV)
-            ops.groupnorm(x, nimg, HW, gamma, beta, 1e-5, 32, silu, out=dst[:, 8:8 + C])
-            outs.append(dst)
-        finally:
-            _lib.check(lib.sdmoe_tune(17, GN_SPLIT_DEFAULT), "tune")
-    assert (outs[0][:, :8] == 7).all() and (outs[0][:, 8 + C:] == 7).all()
+    dst = torch.full((nimg * HW, C + 16), 7.0, dtype=torch.float16, device=DEV)
+    ops.groupnorm(x, nimg, HW, gamma, beta, 1e-5, 32, silu, out=dst[:, 8:8 + C])
+    assert (dst[:, :8] == 7).all() and (dst[:, 8 + C:] == 7).all()
     ref = F.group_norm(x.float().reshape(nimg, HW, C).permute(0, 2, 1), 32, gamma.float(), beta.float(), 1e-5)
     ref = ref.permute(0, 2, 1).reshape(nimg * HW, C)
-    ref = F.silu(ref) if silu else ref
-    close(outs[0][:, 8:8 + C], ref, tol=5e-3)
-    d = (outs[0][:, 8:8 + C].float() - outs[1][:, 8:8 + C].float()).abs()
-    assert d.max().item() <= 2e-3 * max(1.0, ref.abs().max().item())
-    assert (d > 0).float().mean().item() < 1e-3  # the two statistics orders round alike almost everywhere
+    close(dst[:, 8:8 + C], F.silu(ref) if silu else ref, tol=5e-3)
 
 
 @pytest.mark.parametrize("H,C,Cin2,nimg", [(64, 320, 960, 2), (64, 320, 640, 3), (32, 640, 1920, 4), (32, 640, 320, 3),

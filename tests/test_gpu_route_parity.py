@@ -365,7 +365,8 @@ def test_gelu_every_fp16_input_matches_reference_activation(M, gt320):
     vals = torch.zeros(64 * F, dtype=torch.float16)
     vals[:allx.numel()] = allx
     gate = vals.view(64, F)                                   # gate[j, n]: the value row j of x selects
-    ref = torch.nn.functional.gelu(gate)                      # the reference's fp16 GELU (CPU)
+    # the reference's fp16 GELU on the device (the hook runs module.gelu on the GPU gate, moefy.py:13)
+    ref = torch.nn.functional.gelu(gate.to(DEV)).cpu()
     # unfused: y = [value 1.0 | gate]
     y = torch.cat([torch.ones(64, F, dtype=torch.float16), gate], 1).to(DEV)
     g_out = torch.empty((64, F), dtype=torch.float16, device=DEV)

@@ -473,6 +473,12 @@ def test_sdmoe_tune_env_is_parsed_at_load(monkeypatch):
     monkeypatch.setenv("SDMOE_TUNE", "99=1")
     with pytest.raises(_lib.SdmoeError):
         _lib.load()
+    for bad in ("7", "a=1", "1=b", "1=2=3", "=1"):  # malformed entries: SdmoeError, not a bare ValueError
+        monkeypatch.setattr(_lib, "_lib", None)
+        monkeypatch.setenv("SDMOE_TUNE", bad)
+        with pytest.raises(_lib.SdmoeError, match="SDMOE_TUNE"):
+            _lib.load()
+    assert _lib.parse_tune(" 1=0, 16=2,,") == [(1, 0), (16, 2)]
     monkeypatch.setattr(_lib, "_lib", None)
     monkeypatch.delenv("SDMOE_TUNE")
     _lib.load()
@@ -544,46 +550,3 @@ def test_gelu_table_reproduces_reference_activation():
     assert np.all(ulps <= 1.0)
 
 
-def test_step_graph_counter_emulation():
-    """StepGraphs (sdmoe/pipeline.py): the hook owners a replay must emulate are sdmoe receivers without host-side
-    gate capture (anything else disables graphs); each replayed step checks the owners' (timestep, layer) counter
-    against its capture-time value and sets the post-step value, as the eager hooks would."""
-    from sdmoe.pipeline import StepGraphs, hook_owners
-    from neuron_receivers import RemoveExperts, MOEFy
-
-    class Box(torch.nn.Module):
-        def __init__(self):
-            super().__init__()
-            self.a, self.b = torch.nn.Identity(), torch.nn.Identity()
-    unet = Box()
-    rec = RemoveExperts(0, None, 2, 2, expert_indices={t: {l: [] for l in range(2)} for t in range(2)},
-                        store_gates=False)
-    assert hook_owners(unet) == []
-    h1 = unet.a.register_forward_hook(rec.hook_fn)
-    h2 = unet.b.register_forward_hook(rec.hook_fn)
-    assert hook_owners(unet) == [rec]
-    gates = MOEFy(0, store_gates=True)
-    h3 = unet.a.register_forward_hook(gates.hook_fn)
-    assert hook_owners(unet) is None  # gate capture -> no graphs
-    h3.remove()
-    h4 = unet.b.register_forward_hook(lambda m, i, o: o)
-    assert hook_owners(unet) is None  # a foreign hook -> no graphs
-    h4.remove()
-
-    class FakeGraph:
-        def __init__(self, log, i):
-            self.log, self.i = log, i
-
-        def replay(self):
-            self.log.append((self.i, rec.timestep, rec.layer))
-    log = []
-    st = StepGraphs([rec])
-    st.graphs = [FakeGraph(log, 0), FakeGraph(log, 1)]
-    st.counters = [([(0, 0)], [(1, 0)]), ([(1, 0)], [(2, 0)])]
-    rec.reset_time_layer()
-    st.replay()
-    assert log == [(0, 0, 0), (1, 1, 0)] and (rec.timestep, rec.layer) == (2, 0)
-    with pytest.raises(RuntimeError, match="counter"):
-        st.replay()  # not reset: the first step's captured pre-state (0, 0) does not match
-    h1.remove()
-    h2.remove()

@@ -6,7 +6,9 @@ GEGLU call of the first `--steps` DDIM steps, from the fused path's own top-k ke
   * skip_T: the fraction of (T-row tile, 64-neuron K-step) pairs whose keep bits are all zero -- the K-steps
     sdmoe_linear_keep could skip outright;
   * nz_act: nonzero fraction of value*relu(gate) before the top-k mask; nz_kept: after it.
-usage: python tools/expert_union.py [--steps 2] [--out gpurun_out/expert_union.json]"""
+With --model sdxl: SDXL-base 1024^2 (128x128 latents), its own GELU FFN (not relufied), U-Net batch 2 * --batch,
+E = 128 / 256 experts (BASELINE config 5's routing).
+usage: python tools/expert_union.py [--model sd14|sdxl] [--steps 2] [--out gpurun_out/expert_union.json]"""
 import argparse
 import json
 import os
@@ -22,7 +24,8 @@ import torch  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--batch", type=int, default=None, help="prompts (default 8 for sd14, 2 for sdxl: the bench's)")
+    ap.add_argument("--model", choices=("sd14", "sdxl"), default="sd14")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "expert_union.json"))
     a = ap.parse_args()
     from sdmoe.config import UNetConfig
@@ -33,9 +36,13 @@ def main():
     import bench
 
     dev = "cuda:0"
-    cfg = UNetConfig.sd14(64)
+    sdxl = a.model == "sdxl"
+    if a.batch is None:
+        a.batch = 2 if sdxl else 8
+    cfg = UNetConfig.sdxl(128) if sdxl else UNetConfig.sd14(64)
     pipe = StableDiffusionPipeline.synthetic(cfg, seed=0, device=dev, num_inference_steps=50)
-    find_and_change_geglu(pipe.unet)
+    if not sdxl:
+        find_and_change_geglu(pipe.unet)  # relufied SD-1.4; SDXL keeps its GELU (utils.py:111-112)
     moefy_synthetic(pipe, 0.2, 20, seed=0)
     geglus = [m for n, m in pipe.unet.named_modules() if n.endswith("ff.net.0")]
     lists = bench.synth_expert_lists([m.patterns.shape[0] for m in geglus], 50)
@@ -77,11 +84,19 @@ def main():
                 "sel_per_token"):
         summary[key] = {"mean": float(np.mean([r[key] for r in rows])), "min": float(np.min([r[key] for r in rows])),
                         "max": float(np.max([r[key] for r in rows]))}
-    res = {"what": "per hooked GEGLU call, bench routing (SD-1.4 64x64, U-Net batch 16, relu, top-k 0.2, "
-                   "RemoveExperts t<20)", "calls": len(rows), "summary": summary, "per_call": rows}
+    what = ("SDXL-base 128x128, U-Net batch %d, GELU" % (2 * a.batch) if sdxl else
+            "SD-1.4 64x64, U-Net batch %d, relu" % (2 * a.batch))
+    res = {"what": f"per hooked GEGLU call, bench routing ({what}, top-k 0.2, RemoveExperts t<20)",
+           "calls": len(rows), "summary": summary, "per_call": rows}
+    by_e = {}
+    for r in rows:
+        by_e.setdefault(r["E"], []).append(r)
+    res["by_experts"] = {str(E): {key: float(np.mean([r[key] for r in rs])) for key in
+                                  ("union_64", "union_128", "union_256", "skip_64", "skip_128", "skip_256")}
+                         for E, rs in sorted(by_e.items())}
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     json.dump(res, open(a.out, "w"), indent=1)
-    print(json.dumps(summary, indent=1))
+    print(json.dumps({"summary": summary, "by_experts": res["by_experts"]}, indent=1))
 
 
 if __name__ == "__main__":

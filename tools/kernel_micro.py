@@ -23,9 +23,8 @@ def main():
     a = ap.parse_args()
     from sdmoe import _lib
     _lib.check(_lib.load().sdmoe_tune(6, a.diag), "tune")
-    for kv in filter(None, a.tune.split(",")):
-        k, v = kv.split("=")
-        _lib.check(_lib.load().sdmoe_tune(int(k), int(v)), "tune")
+    for k, v in _lib.parse_tune(a.tune):
+        _lib.check(_lib.load().sdmoe_tune(k, v), "tune")
     n, dev = a.nimg, "cuda"
     if a.what == "attn":
         C = 8 * a.d

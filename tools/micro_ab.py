@@ -143,13 +143,11 @@ def main():
     table = {}
     for rep in range(2):  # interleaved twice
         for st in settings:
-            for kv in filter(None, st.split(",")):
-                k, v = kv.split("=")
-                _lib.check(lib.sdmoe_tune(int(k), int(v)), "tune")
+            for k, v in _lib.parse_tune(st):
+                _lib.check(lib.sdmoe_tune(k, v), "tune")
             r = run(cases, a.iters)
-            for kv in filter(None, st.split(",")):  # back to defaults (0) unless the knob's default differs
-                k, _ = kv.split("=")
-                _lib.check(lib.sdmoe_tune(int(k), DEFAULTS.get(k, 0)), "tune")
+            for k, _ in _lib.parse_tune(st):  # back to defaults (0) unless the knob's default differs
+                _lib.check(lib.sdmoe_tune(k, DEFAULTS.get(str(k), 0)), "tune")
             for name, v in r.items():
                 table.setdefault(name, {}).setdefault(st, []).append(v)
     for name, per in table.items():
