@@ -335,8 +335,8 @@ SDMOE_DEV float16v mfma32x32x16(half8 a, half8 b, float16v c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
-template <int D>
-__global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn32_kernel(AttnParams p) {
+template <int D, int NW = 4>
+__global__ __launch_bounds__(NW * 64, (D >= 160 || NW >= 8 ? 1 : 2)) void attn32_kernel(AttnParams p) {
   constexpr int NQC = (D + 15) / 16;                  // 16-deep QK contraction steps (d zero-padded to 16 NQC)
   constexpr int DQ = 16 * NQC;
   constexpr bool SUM_MFMA = (D % 32) != 0 && (D % 4) == 0;  // ones column at d = D inside the last O^T block
@@ -358,7 +358,7 @@ __global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn32_kernel(AttnPar
   constexpr int TILE = KB * RS, TILEV = KB * RSV;
   constexpr int NPK = TILE * 2 / 1024, NPV = TILEV * 2 / 1024;  // 1-KiB LDS-DMA wave-instructions per K / V tile
   static_assert(NPK * 1024 == TILE * 2 && NPV * 1024 == TILEV * 2, "tiles must be whole 1-KiB pieces");
-  constexpr int NPW = (NPK + NPV + 3) / 4;             // per wave (the last round partly empty)
+  constexpr int NPW = (NPK + NPV + NW - 1) / NW;       // per wave (the last round partly empty)
   constexpr int TAIL = 64;                            // zeroed tail behind the K tile
   constexpr int VOFF = TILE + TAIL, SLOT = VOFF + TILEV;
   static_assert(SLV >= 4 * NDB, "V rows hold every column the O^T blocks read");
@@ -375,7 +375,7 @@ __global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn32_kernel(AttnPar
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ln = lane & 31, hf = lane >> 5;           // query column of the MFMA blocks, lane half
   const int b = blockIdx.z, h = blockIdx.y;
-  const int q0 = blockIdx.x * 128 + wave * 32;
+  const int q0 = blockIdx.x * (32 * NW) + wave * 32;
 
   const half_t* Qb = p.Q + (long)b * p.Nq * p.ldq + h * D;
   const half_t* Kb = p.K + (long)b * p.Nk * p.ldk + h * D;
@@ -389,7 +389,7 @@ __global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn32_kernel(AttnPar
   int ldsoff[NPW];
 #pragma unroll
   for (int j = 0; j < NPW; ++j) {
-    const int gp = wave + 4 * j;
+    const int gp = wave + NW * j;
     const bool isk = gp < NPK;
     const int pc = isk ? gp : gp - NPK;
     const int sl = isk ? SL : SLV;
@@ -402,14 +402,14 @@ __global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn32_kernel(AttnPar
   auto issue_tile = [&](half_t* Sd) {
 #pragma unroll
     for (int j = 0; j < NPW; ++j) {
-      if (wave + 4 * j < NPK + NPV) bld16(wave + 4 * j < NPK ? rsK : rsV, Sd + ldsoff[j], voff[j]);
+      if ((NPK + NPV) % NW == 0 || wave + NW * j < NPK + NPV) bld16(wave + NW * j < NPK ? rsK : rsV, Sd + ldsoff[j], voff[j]);
       voff[j] += vstep[j];
     }
   };
 
-  for (int i = tid; i < TAIL; i += 256) S0[TILE + i] = S1[TILE + i] = 0;
+  for (int i = tid; i < TAIL; i += NW * 64) S0[TILE + i] = S1[TILE + i] = 0;
   if constexpr (SUM_MFMA) {
-    for (int i = tid; i < 256; i += 256) {
+    for (int i = tid; i < 256; i += NW * 64) {
       const int u = i / 8;  // 16-B unit; row class r sits at unit (ONES_AT + SLV r) mod 32
       bool one = false;
 #pragma unroll
@@ -484,22 +484,28 @@ __global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn32_kernel(AttnPar
           if (kt * KB + 32 * kb + (r & 3) + 8 * (r >> 2) + 4 * hf >= p.Nk) s[kb][r] = -INFINITY;
     }
     // ---- online softmax, query on the lane: 32 scores here, the other 32 keys in lane ^ 32
-    float m4[8];
+    // lane-local max of the 32 scores: a balanced v_max3 tree (16 instructions); the row max over the lane pair
+    // (l, l ^ 32) only where m is set or moves -- the wave-uniform rescale test needs none (every lane's maximum is
+    // <= THR iff every row's is)
+    auto sv = [&](int i) { return s[i >> 4][i & 15]; };
+    float a1[10];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) m4[i] = max3(s[i >> 2][(i & 3) * 4], s[i >> 2][(i & 3) * 4 + 1], s[i >> 2][(i & 3) * 4 + 2]);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) m4[i] = max2(m4[i], s[i >> 2][(i & 3) * 4 + 3]);
-    float mx = max3(max3(m4[0], m4[1], m4[2]), max3(m4[3], m4[4], m4[5]), max2(m4[6], m4[7]));
-    {
-      auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-      mx = max2(__uint_as_float(r[0]), __uint_as_float(r[1]));
-    }
+    for (int i = 0; i < 10; ++i) a1[i] = max3(sv(3 * i), sv(3 * i + 1), sv(3 * i + 2));
+    const float b0 = max3(a1[0], a1[1], a1[2]), b1 = max3(a1[3], a1[4], a1[5]), b2 = max3(a1[6], a1[7], a1[8]);
+    const float b3 = max3(a1[9], sv(30), sv(31));
+    const float ml = max2(max3(b0, b1, b2), b3);
+    auto xmax = [](float v) {
+      auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+      return max2(__uint_as_float(r[0]), __uint_as_float(r[1]));
+    };
     if constexpr (FIRST) {  // first tile: m = its max (O and l are still zero)
+      const float mx = xmax(ml);
       mrun = ONES_K ? (float)(half_t)mx : mx;
       set_shift(mrun);
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) s[kb] -= mrun;
-    } else if (!__all(mx <= RESCALE_THR)) {  // wave-uniform: deferred rescale (p <= 2^8 keeps fp16 safe)
+    } else if (!__all(ml <= RESCALE_THR)) {  // wave-uniform: deferred rescale (p <= 2^8 keeps fp16 safe)
+      const float mx = xmax(ml);
       const float mnew = ONES_K ? (float)(half_t)(mrun + fmaxf(mx, 0.f)) : mrun + fmaxf(mx, 0.f);
       const float delta = mnew - mrun;  // exact: the shifts old and new are both in use as given
       mrun = mnew;
@@ -596,7 +602,7 @@ __global__ __launch_bounds__(256, (D >= 160 ? 1 : 2)) void attn32_kernel(AttnPar
 // sdmoe_tune knob 4: 0 = by shape (default): attn32_kernel for d = 80 self-attention (Nk > 128), the 16x16x32 kernel
 // in 8-wave workgroups for d = 40 / 64 self-attention (Nk > 128), the 4-wave 16x16x32 kernel (NQF = 2) everywhere
 // else; 1 = attn32_kernel; 2 or 4 = the 4-wave 16x16x32 kernel with NQF = 2 / 4; 8 = the 16x16x32 kernel in
-// 8-wave workgroups (d <= 80)
+// 8-wave workgroups (d <= 80); 9 = attn32_kernel in 8-wave workgroups (d <= 80)
 int g_attn_nqf = 0;
 
 template <int D>
@@ -616,7 +622,10 @@ int launch(const AttnParams& p, int nimg, hipStream_t s) {
   // self-attentions at d = 40 / 64: d = 40 N = 4096 448 vs 464-475 us, pipeline +0.5 % (same box); slower on the
   // 77-key cross-attention (34.4 vs 31.1 us: fewer workgroups) and at d = 80 (65.4 vs 62.4 us with attn32)
   const bool use8 = g_attn_nqf == 8 || (g_attn_nqf == 0 && (D == 40 || D == 64) && p.Nk > 128);
-  if (use32) {
+  if (g_attn_nqf == 9 && D <= 80) {  // 32x32x16 kernel in 8-wave workgroups
+    dim3 grid((p.Nq + 255) / 256, p.heads, nimg);
+    attn32_kernel<D, (D <= 80 ? 8 : 4)><<<grid, (D <= 80 ? 512 : 256), 0, s>>>(p);
+  } else if (use32) {
     dim3 grid((p.Nq + 127) / 128, p.heads, nimg);
     attn32_kernel<D><<<grid, 256, 0, s>>>(p);
   } else if (WIDE_OK && wide) {
@@ -636,7 +645,7 @@ int launch(const AttnParams& p, int nimg, hipStream_t s) {
 }  // namespace
 
 int sdmoe_attn_set_nqf(int v) {
-  if (v != 0 && v != 1 && v != 2 && v != 4 && v != 8) return SDMOE_EARG;
+  if (v != 0 && v != 1 && v != 2 && v != 4 && v != 8 && v != 9) return SDMOE_EARG;
   g_attn_nqf = v;
   return SDMOE_OK;
 }

@@ -569,12 +569,18 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
     }
     const unsigned boff = (unsigned)(fr * RB + ((fg ^ swzk(fr)) << 4));
     const int orow_w = (wr * WM) / HW_;  // the wave's first output row within the tile
-    // MFMAs of one K-step: A fragment i from a_at(i), B fragments from sb
-    auto mfma_step = [&](const char* sb, auto&& a_at) {
+    // MFMAs of one K-step: A fragment i from a_at(i), B fragments from sb. pre() (the K-step's LDS-DMA issue) runs
+    // after the first fragment reads are issued: the DMA issue (~60 cycles per piece) then overlaps the reads' LDS
+    // latency instead of delaying them behind the barrier
+    auto mfma_step = [&](const char* sb, auto&& a_at, auto&& pre) {
       half8 bcur[FN];
 #pragma unroll
       for (int j = 0; j < FN; ++j) bcur[j] = *reinterpret_cast<const half8*>(sb + boff + 16 * j * RB);
       half8 a0 = a_at(0), a1 = a_at(1);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("" ::: "memory");  // keeps the reads ahead of the DMA issue (IR-level code motion)
+      pre();
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int g = 0; g < FM / 2; ++g) {
         half8 n0 = a0, n1 = a1;
@@ -661,10 +667,12 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
         vm_wait(nwait);
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (ks + 2 < nkl && !(p.diag & 1)) issue_group(ks + 2);
-        if (t == 0 && more && !(p.diag & 1)) issue_halo(c_first + cs + 1, hb ^ 1);
+        auto pre = [&]() {
+          if (ks + 2 < nkl && !(p.diag & 1)) issue_group(ks + 2);
+          if (t == 0 && more && !(p.diag & 1)) issue_halo(c_first + cs + 1, hb ^ 1);
+        };
         if (t == 5 && more && gn) transform(c_first + cs + 1, hb ^ 1);
-        if (p.diag & 2) return;
+        if (p.diag & 2) { pre(); return; }
         mfma_step(bbase + (t % 3) * BSTAGE + wc * WN * RB, [&](int i) -> half8 {
           const int i16 = 16 * i;
           if constexpr (HUP)  // input row ((orow + kh - 1) >> 1) - (oh0 / 2 - 1), column (ocol0 / 2) + lane part
@@ -672,7 +680,7 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
                                                    (((((i16 / HW_) + kh - 1) >> 1) + 1) * HP + (i16 % HW_) / 2) * RB);
           else
             return *reinterpret_cast<const half8*>(hbuf + aoff[kw] + ((i16 / HW_ + kh) * HP + (i16 % HW_) + kw) * RB);
-        });
+        }, pre);
       };
       tap_step(std::integral_constant<int, 0>());
       tap_step(std::integral_constant<int, 1>());
@@ -689,12 +697,14 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
       vm_wait(ks + 1 < nkl ? group_cnt(ks + 1) : 0);
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      if (ks + 2 < nkl && !(p.diag & 1)) issue_group(ks + 2);
-      if (p.diag & 2) continue;
+      auto pre = [&]() {
+        if (ks + 2 < nkl && !(p.diag & 1)) issue_group(ks + 2);
+      };
+      if (p.diag & 2) { pre(); continue; }
       const char* a2s = hbase + ((nsl + (slot == 2 ? 1 : 0)) & 1) * HBYTES + (slot == 1 ? A2BYTES : 0) + wr * WM * RB;
       mfma_step(bbase + slot * BSTAGE + wc * WN * RB, [&](int i) -> half8 {
         return *reinterpret_cast<const half8*>(a2s + boff + 16 * i * RB);
-      });
+      }, pre);
     }
   } else {
   // prologue: stages 0 .. NSTAGE-2

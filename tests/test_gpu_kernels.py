@@ -264,13 +264,13 @@ def test_attention(d, Nq, Nk):
     close(out, ref)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 4, 8, 16, 40])
+@pytest.mark.parametrize("variant", [1, 2, 4, 8, 9])
 @pytest.mark.parametrize("d,Nq,Nk", [(40, 256, 256), (40, 300, 77), (80, 200, 200), (64, 300, 300),
                                      (32, 130, 130), (40, 64, 50), (40, 1000, 4096), (40, 520, 128)])
 def test_attention_forced_variant(variant, d, Nq, Nk):
     """Every attention kernel variant (sdmoe_tune knob 4: 1 = 32x32x16 kernel, 2 / 4 = 16x16x32 kernel with 32 / 64
-    queries per wave, 8 = 16x16x32 kernel in 8-wave workgroups), ragged Nq and Nk, single-tile and exactly-whole-tile
-    key counts."""
+    queries per wave, 8 = 16x16x32 kernel in 8-wave workgroups, 9 = 32x32x16 kernel in 8-wave workgroups), ragged Nq
+    and Nk, single-tile and exactly-whole-tile key counts."""
     from sdmoe import _lib
     lib = _lib.load()
     nimg, heads = 2, 4
@@ -290,7 +290,7 @@ def test_attention_forced_variant(variant, d, Nq, Nk):
     close(out, ref)
 
 
-@pytest.mark.parametrize("d,variant", [(80, 0), (40, 0), (40, 8)])
+@pytest.mark.parametrize("d,variant", [(80, 0), (40, 0), (40, 8), (40, 9), (40, 1)])
 def test_attention_peaked_softmax(d, variant):
     """A spiked key forces the online-softmax rescale branch at a later tile."""
     from sdmoe import _lib
