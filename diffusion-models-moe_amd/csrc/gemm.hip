@@ -32,6 +32,10 @@ int g_bk = 0;
 int g_res16 = 1;  // knob 8: 1 = residual epilogues on the fp16 staging path (residual added in the copy-out), 0 = fp32
 int g_ksplit = 0;  // knob 9: forced split-K factor (0 = auto; 1 = never split), for tile sweeps
 int g_mfast = 1;   // knob 14: split-K conv grids ordered M-tile fastest (1) or split fastest (0)
+// knob 23: fp16 epilogues storing 16-B row pieces straight from the fragments (no LDS staging): 1 (default) = when
+// there is no residual (LN-folded projections 4-12 %, plain K = 320 linears ~3 % faster; with a residual its 16-B
+// residual loads measured 3-7 % slower than the staged copy-out), 2 = always, 0 = never
+int g_epi_direct = 1;
 int g_diag = 0;  // knob 6, diagnostics only (results garbage): bit 0 = no K-loop operand loads, bit 1 = no MFMAs,
                  // bit 4 = no A-operand pieces, bit 5 = no B-operand pieces,
                  // bit 2 = no epilogue (nothing stored), bit 3 = epilogue without its global stores
@@ -62,6 +66,7 @@ struct GemmParams {
   int esize;
   int res16;  // residual on the fp16 staging path (sdmoe_tune knob 8)
   int diag;  // diagnostic knob (sdmoe_tune 6): bit 0 skips the K-loop loads, bit 1 the MFMAs
+  int epi_direct;  // fp16 epilogue: stores straight from the fragments instead of LDS staging (knob 23 policy)
   // expert keep mask of the A operand (MODE_KEEP / MODE_KEEPW): keep[(k / 64) * M * 8 + m * 8 + (k % 64) / 8] bit
   // (k % 8) = neuron k of token m survives the top-k; the A fragments are ANDed with it after their LDS read
   const uint8_t* keep;
@@ -727,8 +732,18 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
     }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (it + NSTAGE - 1 < nk && !(p.diag & 1)) issue_stage(ks0 + it + NSTAGE - 1, (it + NSTAGE - 1) % NSTAGE);
-    else if (TAB_PREFETCH && it == nk - 1) issue_gelu_tab(smem + (nk % NSTAGE) * STAGE + STAGE - TAB_BYTES);
+    // the next stage's LDS-DMA (into the slot read in step it - 1, which every wave finished before the barrier).
+    // 3-stage rings: issued after this step's first fragment reads, so its ~60 issue cycles per piece overlap their
+    // LDS latency instead of delaying the first MFMA behind the barrier. 2-stage rings keep it right behind the
+    // barrier: their stage has one K-step to land, and the later issue measured 2-5 % slower there (routed GEGLU,
+    // 128x160 convs, K = 5120 projections; r05f)
+    auto issue_next = [&]() {
+      if (it + NSTAGE - 1 < nk && !(p.diag & 1)) issue_stage(ks0 + it + NSTAGE - 1, (it + NSTAGE - 1) % NSTAGE);
+      else if (TAB_PREFETCH && it == nk - 1) issue_gelu_tab(smem + (nk % NSTAGE) * STAGE + STAGE - TAB_BYTES);
+    };
+    constexpr bool PIPE = !(KEEP && FN > 5);
+    constexpr bool LATE_DMA = PIPE && NSTAGE >= 3;
+    if (!LATE_DMA || (p.diag & 2)) issue_next();
 
     const char* sa = smem + (it % NSTAGE) * STAGE;
     const char* sbm = sa + BM * BK * 2;
@@ -760,7 +775,7 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
       }
       return b;
     };
-    if constexpr (!(KEEP && FN > 5)) {  // (wide masked tiles: no registers to spare)
+    if constexpr (PIPE) {  // (wide masked tiles: no registers to spare)
       // software-pipelined: A fragments in pairs, the next pair's LDS reads issued before the current pair's
       // 2*FN MFMAs (one group of latency cover); the next kk's B fragments read during the last group when they
       // fit a second register set. sched_barrier pins the read / MFMA order so hipcc cannot sink the reads to
@@ -772,6 +787,12 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
 #pragma unroll
       for (int j = 0; j < FN; ++j) bcur[j] = read_b(0, j);
       half8 a0 = read_a(0, 0), a1 = read_a(0, 1);
+      if constexpr (LATE_DMA) {
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("" ::: "memory");
+        issue_next();
+        __builtin_amdgcn_sched_barrier(0);
+      }
 #pragma unroll
       for (int kk = 0; kk < NKK; ++kk) {
 #pragma unroll
@@ -897,6 +918,85 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
     for (int j = 0; j < FN; ++j) {
       const int n = nw + 16 * j + 4 * fg;
       b4[j] = (!LN && p.bias && n < p.N) ? *reinterpret_cast<const half4*>(p.bias + n) : (half4){0, 0, 0, 0};
+    }
+    if (!WKEEP && p.epi_direct) {  // (the Wanda-masked tiles: no registers to spare for it)
+      // Direct fp16 stores, no LDS staging (sdmoe_tune knob 23): per fragment row and pair of fragments (j, j + 1)
+      // two v_permlane16_swap per lane leave each lane 8 consecutive output columns of its row -- lane group g:
+      // fragment j + (g & 1), columns 8 (g >> 1) .. +7 -- stored as one 16-B piece (the T21 widening on the 16x16
+      // fragment layout); an unpaired last fragment stores 8 B per lane. Residual: loaded in the same layout and added
+      // to the fp16-rounded output in fp16 arithmetic, as the staged path.
+      const bool res = p.R != nullptr;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        __builtin_amdgcn_sched_barrier(0);
+        const int m = mw + 16 * i + fr;
+        const half_t* cap = (p.coladd && m < p.M) ? p.coladd + (long)(m / p.rows_per_batch) * p.coladd_bstride : nullptr;
+        const float* cfp = (p.colf && m < p.M) ? p.colf + (long)(m / p.rows_per_batch) * p.colf_bstride : nullptr;
+        float a = 0.f, c = 0.f;
+        if constexpr (LN) {
+          const int rl = wr * WM + 16 * i + fr;
+          a = ln_row[2 * rl];
+          c = ln_row[2 * rl + 1];
+        }
+        auto frag16 = [&](int j) -> uint2v {  // fragment j of row block i: + bias / column adds (/ LN), rounded
+          const int n = nw + 16 * j + 4 * fg;
+          float4v v = acc[i][j];
+          if constexpr (LN) {
+            const int cl = wc * WN + 16 * j + 4 * fg;
+            const float4v ws = *reinterpret_cast<const float4v*>(ln_col + cl);
+            const float4v lb = *reinterpret_cast<const float4v*>(ln_col + BN + cl);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = __builtin_fmaf(a, v[r], __builtin_fmaf(c, ws[r], lb[r]));
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += (float)b4[j][r];
+          if (cap && n < p.N) {
+            const half4 cc = *reinterpret_cast<const half4*>(cap + n);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += (float)cc[r];
+          }
+          if (cfp && n < p.N) {
+            const float4v cc = *reinterpret_cast<const float4v*>(cfp + n);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += cc[r];
+          }
+          half4 y;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) y[r] = (half_t)v[r];
+          return __builtin_bit_cast(uint2v, y);
+        };
+#pragma unroll
+        for (int j = 0; j + 1 < FN; j += 2) {
+          const uint2v ya = frag16(j), yb = frag16(j + 1);
+          const auto s0 = __builtin_amdgcn_permlane16_swap(ya[0], yb[0], false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(ya[1], yb[1], false, false);
+          const int n = nw + 16 * (j + (fg & 1)) + 8 * (fg >> 1);
+          half8 o = __builtin_bit_cast(half8, (uint4v){s0[0], s1[0], s0[1], s1[1]});
+          if (m < p.M && n < p.N) {
+            if (res) {
+              const half8 rr = *reinterpret_cast<const half8*>(p.R + (long)m * p.ldr + n);
+#pragma unroll
+              for (int r = 0; r < 8; ++r) o[r] = (half_t)((float)o[r] + (float)rr[r]);
+            }
+            if (p.diag & 8) asm volatile("" ::"v"(o));
+            else *reinterpret_cast<half8*>(p.C + (long)m * p.ldc + n) = o;
+          }
+        }
+        if constexpr (FN % 2) {
+          const int n = nw + 16 * (FN - 1) + 4 * fg;
+          half4 o = __builtin_bit_cast(half4, frag16(FN - 1));
+          if (m < p.M && n < p.N) {
+            if (res) {
+              const half4 rr = *reinterpret_cast<const half4*>(p.R + (long)m * p.ldr + n);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) o[r] = (half_t)((float)o[r] + (float)rr[r]);
+            }
+            if (p.diag & 8) asm volatile("" ::"v"(o));
+            else *reinterpret_cast<half4*>(p.C + (long)m * p.ldc + n) = o;
+          }
+        }
+      }
+      return;
     }
     half_t* st = reinterpret_cast<half_t*>(smem) + wave * (WM / NPASS16) * RS16;
     // residual (fp16, 16-B row chunks): this pass's chunks are loaded before its accumulators are staged, so their
@@ -1164,6 +1264,16 @@ int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s, int ks_w
     ksplit = g_ksplit > 0 ? g_ksplit : ks_want;
     if (ksplit > nk) ksplit = nk;
     while (ksplit > 1 && (long)ksplit * p.M * p.N > ws_floats) --ksplit;
+  } else if (ws && (MODE == MODE_CONV || MODE == MODE_CONV_UP) && ntiles <= 16 && nk >= 64) {
+    // latency regime (one prompt per call, base_receiver.py:73: 8x8 / 16x16 / 32x32 convs at batch 2): up to two
+    // workgroups per CU, >= 11 K-steps per split, <= 64 MB of fp32 slabs -- B = 1 sweep (profiles/r05_b1_split_sweep.txt):
+    // 8x8 1280 -> 1280 28.1 -> 23.5 us, 2560 -> 1280 44.3 -> 29.6, 16x16 stride 2 39.9 -> 22.0, 32x32 1280 -> 640
+    // 64.2 -> 55.2 (at most 8 splits before)
+    ksplit = (512 + ntiles - 1) / ntiles;
+    if (ksplit > 24) ksplit = 24;
+    if (ksplit > nk / 11) ksplit = nk / 11;
+    while (ksplit > 1 && (long)ksplit * p.M * p.N * 4 > (64L << 20)) --ksplit;
+    while (ksplit > 1 && (long)ksplit * p.M * p.N > ws_floats) --ksplit;
   } else if (ws && ntiles < 192 && nk >= 16) {
     ksplit = (256 + ntiles - 1) / ntiles;
     if (ksplit > 8) ksplit = 8;
@@ -1179,6 +1289,7 @@ int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s, int ks_w
   // measured 2 us slower with it
   p.mfast = (p.ksplit > 1 && g_mfast && (MODE == MODE_CONV || MODE == MODE_CONV_UP)) ? 1 : 0;
   p.diag = g_diag;
+  p.epi_direct = g_epi_direct == 2 || (g_epi_direct == 1 && p.R == nullptr);  // host-side: a device test of R spilled
   p.res16 = g_res16;
   const dim3 grid(ntiles * p.ksplit);
   {
@@ -1224,7 +1335,20 @@ int launch_halo(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
   const int ntiles = (p.M / BM) * (p.N / 320);
   const int nsl = p.Cin / 32;
   int ksplit = 1;
-  if (ws && ntiles < 200) {
+  if (ws && g_ksplit > 0) {  // forced (knob 9, sweeps): at most one 32-channel slice per split
+    ksplit = g_ksplit < nsl ? g_ksplit : nsl;
+    while (ksplit > 1 && (long)ksplit * p.M * p.N > ws_floats) --ksplit;
+  } else if (ws && ntiles <= 32) {
+    // latency regime (batch 2: whole 16x16 images, the 8 -> 16 upsample, 64x64 at 32 tiles): up to two workgroups
+    // per CU, >= 2 slices per split, <= 96 MB of fp32 slabs -- B = 1 sweep: 16x16 1280 -> 1280 56.1 -> 40.9 us
+    // (20 splits), 2560 -> 1280 91.7 -> 55.3, 8 -> 16 upsample 38.0 -> 31.7 (at most 8 splits before)
+    ksplit = (512 + ntiles - 1) / ntiles;
+    if (ksplit > 32) ksplit = 32;
+    if (ksplit > nsl / 2) ksplit = nsl / 2;
+    while (ksplit > 1 && (long)ksplit * p.M * p.N * 4 > (96L << 20)) --ksplit;
+    while (ksplit > 1 && (long)ksplit * p.M * p.N > ws_floats) --ksplit;
+    if (ksplit < 1) ksplit = 1;
+  } else if (ws && ntiles < 200) {
     ksplit = (256 + ntiles - 1) / ntiles;  // 6 / 8 splits: 172 vs 128 us at 16x16 x 1280 (r04)
     if (ksplit > 8) ksplit = 8;
     if (ksplit > nsl / 2) ksplit = nsl / 2;
@@ -1238,6 +1362,7 @@ int launch_halo(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
   p.part = p.ksplit > 1 ? ws : nullptr;
   p.mfast = p.ksplit > 1 ? g_mfast : 0;
   p.diag = g_diag;
+  p.epi_direct = g_epi_direct == 2 || (g_epi_direct == 1 && p.R == nullptr);  // host-side: a device test of R spilled
   p.res16 = g_res16;
   (void)HW_;
   gemm_kernel<BM, 320, 2, 4, MODE, 3, 32><<<dim3(ntiles * p.ksplit), 512, 0, s>>>(p);
@@ -1810,7 +1935,7 @@ extern "C" int sdmoe_tune(int knob, int value) {
   if (knob == 7) return sdmoe_gn_set_fused(value);
   if (knob == 0 && (value == 0 || value == 2 || value == 3)) { g_stages = value; return SDMOE_OK; }
   if (knob == 1 && value >= 0 && value <= 8) { g_tile = value; return SDMOE_OK; }
-  if (knob == 9 && value >= 0 && value <= 16) { g_ksplit = value; return SDMOE_OK; }
+  if (knob == 9 && value >= 0 && value <= 32) { g_ksplit = value; return SDMOE_OK; }
   if (knob == 14 && (value == 0 || value == 1)) { g_mfast = value; return SDMOE_OK; }
   if (knob == 2 && (value == 0 || value == 32 || value == 64)) { g_bk = value; return SDMOE_OK; }
   if (knob == 6 && value >= 0 && value <= 63) { g_diag = value; return SDMOE_OK; }
@@ -1819,5 +1944,6 @@ extern "C" int sdmoe_tune(int knob, int value) {
   if (knob == 16 && value >= 0 && value <= 3) { g_halo = value; return SDMOE_OK; }
   if (knob == 20 && (value == 0 || value == 1)) { g_gt320 = value; return SDMOE_OK; }
   if (knob == 21 && (value == 0 || value == 1)) { g_narrow = value; return SDMOE_OK; }
+  if (knob == 23 && value >= 0 && value <= 2) { g_epi_direct = value; return SDMOE_OK; }
   return SDMOE_EARG;
 }

@@ -505,29 +505,33 @@ class Routing:
         return cls(labels, E, k, device or patterns.device)
 
 
+def geglu_rows(F: int, perm: torch.Tensor | None, device) -> torch.Tensor:
+    """Source row of proj.weight [2F, K] (value rows, then gate rows) for every row of the layout sdmoe_linear_geglu
+    reads (include/sdmoe.h): neurons permuted by `perm`, value and gate rows interleaved per neuron pair [v 2 | g 2]
+    (rows 4 q .. 4 q + 3 = value 2 q, value 2 q + 1, gate 2 q, gate 2 q + 1), so each lane of the kernel's swapped
+    MFMA fragments holds both halves of two neurons."""
+    if F % 2:
+        raise ValueError(f"GEGLU layout: F = {F} is odd")
+    idx = torch.arange(F, device=device) if perm is None else perm.to(device)
+    r = torch.arange(2 * F, device=device)
+    q, e = r // 4, r % 4
+    c = 2 * q + (e & 1)
+    return torch.where(e < 2, idx[c], F + idx[c])
+
+
 def interleave_geglu(weight: torch.Tensor, bias: torch.Tensor | None, perm: torch.Tensor | None):
-    """proj.weight [2F, K] (value rows, then gate rows) -> rows permuted by `perm` and interleaved [v 2 | g 2]
-    per neuron pair (rows 4 q .. 4 q + 3 = value 2q, value 2q+1, gate 2q, gate 2q+1), the layout sdmoe_linear_geglu
-    reads: each lane of its swapped MFMA fragments then holds both halves of two neurons. bias likewise (zeros if
-    None)."""
+    """proj.weight [2F, K] -> rows in geglu_rows' order (neurons permuted by `perm`), the layout sdmoe_linear_geglu
+    reads; bias likewise (zeros if None)."""
     F2, K = weight.shape
-    F = F2 // 2
-    idx = torch.arange(F, device=weight.device) if perm is None else perm.to(weight.device)
-    wv, wg = weight[:F][idx], weight[F:][idx]
-    w_il = torch.stack([wv.view(F // 2, 2, K), wg.view(F // 2, 2, K)], 1).reshape(F2, K).contiguous()
+    rows = geglu_rows(F2 // 2, perm, weight.device)
     b = torch.zeros(F2, dtype=weight.dtype, device=weight.device) if bias is None else bias
-    bv, bg = b[:F][idx], b[F:][idx]
-    b_il = torch.stack([bv.view(F // 2, 2), bg.view(F // 2, 2)], 1).reshape(F2).contiguous()
-    return w_il, b_il
+    return weight[rows].contiguous(), b[rows].contiguous()
 
 
 def interleave_ln_fold(fold: LNFold, perm: torch.Tensor | None) -> LNFold:
     """An LNFold of proj.weight [2F, K] with its rows in interleave_geglu's order."""
     F = fold.w.shape[0] // 2
-    dev = fold.w.device
-    idx = torch.arange(F, device=dev) if perm is None else perm.to(dev)
-    rows = torch.stack([idx.view(F // 2, 2), (idx + F).view(F // 2, 2)], 1).reshape(2 * F)
-    return fold.rows(rows)
+    return fold.rows(geglu_rows(F, perm, fold.w.device))
 
 
 _GELU_TABLES = {}

@@ -186,7 +186,8 @@ int sdmoe_geglu_route(const void* Y, long ldy, int M, int F, int E, int k, int a
  *  1. sdmoe_linear_geglu: P[m, n] = fp16(fp16(x W_v^T + b_v) * fp16(act(fp16(x W_g^T + b_g)))) for all F neurons
  *     and score[m, e] = fp16(sum over expert e's neurons of act(gate)) in the GEMM epilogue. W [2F, K] / bias
  *     [2F] hold the neurons permuted so every expert is contiguous (expert-major, ascending neuron id), value
- *     and gate rows interleaved in pairs ([v 2 | g 2] per neuron pair). F % 80 == 0. score may be NULL
+ *     and gate rows interleaved in pairs ([v 2 | g 2] per neuron pair, sdmoe/ops.py geglu_rows). F % 80 == 0. score
+ *     may be NULL
  *     (dense GEGLU). Same rounding points as sdmoe_linear + sdmoe_geglu_route.
  *  2. sdmoe_moe_topk_mask: per token, removed experts score 0, top-k (ties toward the lowest expert id) and
  *     zero every neuron of P whose expert is not selected or removed. sel_out as above (may be NULL).
@@ -347,7 +348,7 @@ int sdmoe_cfg_multistep_step(const void* eps, long lde, float* lat, int B, int H
 /* Tuning knobs for A/B experiments: knob 0 = GEMM LDS pipeline stages (0 auto, 2 or 3); knob 1 = forced GEMM tile
    (0 auto, 1 = 128x160, 2 = 64x160, 3 = 256x320 8-wave, 4 = 256x160 8-wave, 5 = 256x320 4x2-wave, 6 = 128x320 8-wave,
    7 = 128x160 8-wave, 8 = 64x320 8-wave; 7/8 plain GEMM / conv / LN-folded GEMM only); knob 9 = forced split-K
-   factor (0 auto, 1 = never split, 2..16); knob 14 = split-K conv tile order: 1 (default) M-tile fastest (one XCD's
+   factor (0 auto, 1 = never split, 2..32; halo convs: at most one 32-channel slice per split); knob 14 = split-K conv tile order: 1 (default) M-tile fastest (one XCD's
    workgroups share weight slices in its L2), 0 split fastest; knob 2 = K-step
    depth (0 auto, 32, 64); knob 4 = attention kernel (0 auto by shape,
    1 = 32x32x16 MFMA kernel, 2 / 4 = 4-wave 16x16x32 kernel with 32 / 64 queries per wave, 64 for head_dim <= 40
@@ -362,7 +363,9 @@ int sdmoe_cfg_multistep_step(const void* eps, long lde, float* lat, int B, int H
    knob 16 = halo-tiled 3x3 convs: 1 (default) where measured faster (64- and 16-wide outputs, the upsample convs),
    2 = every 128-row halo tile instead, 3 = the default plus 32-wide outputs on 256-row tiles, 0 = off;
    knob 20 = table-GELU routed GEGLU tiles: 1 (default) 256x320 like the ReLU kernel, 0 = 256x160 (4x2 waves);
-   knob 21 = convs with at most 32 output channels (conv_out): 1 (default) 128x32 tiles, 0 = 128x64. */
+   knob 21 = convs with at most 32 output channels (conv_out): 1 (default) 128x32 tiles, 0 = 128x64;
+   knob 23 = fp16 GEMM / conv epilogues: 1 (default) 16-B row pieces stored straight from the MFMA fragments (two
+   v_permlane16_swap per fragment pair, no LDS staging) when there is no residual, 2 = always, 0 = staged in LDS. */
 int sdmoe_tune(int knob, int value);
 
 /*

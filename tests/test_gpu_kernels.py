@@ -701,3 +701,55 @@ def test_conv3x3_folded_shortcut(H, C, Cin2, nimg):
     ref = ref + x.float() @ wsc.float().t() + cadd.float().repeat_interleave(H * H, 0)
     close(out, ref)
 
+
+
+@pytest.mark.parametrize("kind", ["linear", "linear_res", "linear_ln", "conv_temb", "conv_halo_sc", "keep", "per_image"])
+def test_direct_epilogue_bit_identical(kind):
+    """fp16 epilogue stored straight from the MFMA fragments (sdmoe_tune knob 23 = 2: two v_permlane16_swap per
+    fragment pair, 16-B row pieces) vs the LDS-staged copy-out (knob 23 = 0): bit-identical outputs, M / N tails,
+    strided output views; the default (1) takes the direct path only without a residual."""
+    g = 16
+    outs = []
+
+    def run():
+        if kind in ("linear", "linear_res"):
+            M, N, K = 1000, 968, 320
+            x, w, b = rnd(M, K, seed=g), rnd(N, K, scale=K ** -0.5, seed=g + 1), rnd(N, scale=0.1, seed=g + 2)
+            r = rnd(M, N, seed=g + 3) if kind == "linear_res" else None
+            dst = torch.full((M, N + 24), 3.0, dtype=torch.float16, device=DEV)
+            ops.linear(x, w, b, residual=r, out=dst[:, 8:8 + N])
+            return dst
+        if kind == "linear_ln":
+            M, N, K = 777, 640, 320
+            x = rnd(M, K, seed=g) * 2 + 1
+            w, b = rnd(N, K, scale=K ** -0.5, seed=g + 1), rnd(N, scale=0.1, seed=g + 2)
+            gamma, beta = rnd(K, scale=0.1, seed=g + 3) + 1, rnd(K, scale=0.1, seed=g + 4)
+            fold = ops.LNFold(w, gamma, beta, 1e-5, bias=b)
+            return ops.linear_ln(x, fold)
+        if kind == "conv_temb":
+            nimg, H, C = 3, 32, 640
+            x = rnd(nimg * H * H, C, seed=g)
+            w, b = rnd(C, 3, 3, C, scale=(9 * C) ** -0.5, seed=g + 1), rnd(C, scale=0.1, seed=g + 2)
+            temb = rnd(nimg, C, seed=g + 3)
+            return ops.conv3x3(x, nimg, H, H, ops.conv_weight(w), b, coladd=temb, coladd_bstride=C)
+        if kind == "conv_halo_sc":
+            nimg, H, C, C2 = 2, 64, 320, 640
+            x, x2 = rnd(nimg * H * H, C, seed=g), rnd(nimg * H * H, C2, seed=g + 5)
+            w, w2 = rnd(C, 3, 3, C, scale=(9 * C) ** -0.5, seed=g + 1), rnd(C, C2, scale=C2 ** -0.5, seed=g + 6)
+            wc = ops.conv_weight_with_shortcut(ops.conv_weight(w), w2)
+            return ops.conv3x3(x, nimg, H, H, wc, rnd(C, scale=0.1, seed=g + 2), shortcut=x2)
+        if kind == "keep":
+            M, F, N, E = 4096, 1280, 320, 64
+            routing = ops.Routing(torch.arange(F) % E, E, E // 5, DEV)
+            keep = ops.moe_topk_keep(rnd(M, E, seed=g), routing, M)
+            return ops.linear_keep(rnd(M, F, seed=g + 1), keep, rnd(N, F, scale=F ** -0.5, seed=g + 2),
+                                   rnd(N, scale=0.1, seed=g + 3))
+        nimg, HW, N, K = 4, 256, 320, 320  # per_image (GN-folded proj_in)
+        x = rnd(nimg * HW, K, seed=g)
+        wf = rnd(nimg, N, K, scale=K ** -0.5, seed=g + 1)
+        colf = rnd(nimg, N, seed=g + 3).float()
+        return ops.linear_per_image(x, wf, colf, HW)
+
+    for mode in (0, 2, 1):
+        _with_tune([(23, mode)], lambda: outs.append(run()))
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])

@@ -550,3 +550,22 @@ def test_gelu_table_reproduces_reference_activation():
     assert np.all(ulps <= 1.0)
 
 
+
+
+def test_geglu_rows_layout():
+    """sdmoe_linear_geglu's weight layout (ops.geglu_rows, include/sdmoe.h): rows 4 q .. 4 q + 3 = value 2 q, value
+    2 q + 1, gate 2 q, gate 2 q + 1 of the (permuted) neurons; a permutation of all 2F rows."""
+    from sdmoe import ops
+    F = 120
+    rows = ops.geglu_rows(F, None, "cpu")
+    assert sorted(rows.tolist()) == list(range(2 * F))
+    for r in range(2 * F):
+        q, e = divmod(r, 4)
+        c = 2 * q + (e & 1)
+        assert rows[r].item() == (c if e < 2 else F + c)
+    perm = torch.randperm(F, generator=torch.Generator().manual_seed(5))
+    rp = ops.geglu_rows(F, perm, "cpu")
+    assert torch.equal(rp, torch.where(rows < F, perm[rows % F], F + perm[rows % F]))
+    w = torch.randn(2 * F, 8)
+    w_il, _ = ops.interleave_geglu(w, None, perm)
+    assert torch.equal(w_il[0], w[perm[0]]) and torch.equal(w_il[2], w[F + perm[0]]) and torch.equal(w_il[5], w[perm[3]])
