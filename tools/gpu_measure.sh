@@ -47,6 +47,13 @@ for s in $STEPS; do
       f=$(find $O/$s -name '*kernel_stats.csv' 2>/dev/null | head -1)
       [ -n "$f" ] && python tools/prof_summary.py $f 45 > $O/${s}_summary.txt && cp $f $O/${s}_kernel_stats.csv && head -14 $O/${s}_summary.txt
       rm -rf $O/$s ;;  # the raw traces would push gpurun_out past the 64 MiB copy-back limit
+    trace|trace_b1)  # one denoising step's dispatch sequence (durations, gaps, grids) -> ${s}_seq.txt
+      [ $s = trace_b1 ] && bb="--batch 1" || bb=""
+      cd /tmp && export TMPDIR=/tmp
+      step $s 600 rocprofv3 --kernel-trace -d $O/$s -o run --output-format csv -- python3 $R/bench.py $bb --inference-steps 3 --steps 1 --warmup 0 --no-cpu-baseline --no-roofline --e2e-steps 0
+      cd $R
+      python tools/trace_seq.py $(find $O/$s -name '*kernel_trace.csv' | head -1) --out $O/${s}_seq.txt > /dev/null && head -3 $O/${s}_seq.txt
+      rm -rf $O/$s ;;
     pmc)
       cd /tmp && export TMPDIR=/tmp
       for c in FETCH_SIZE WRITE_SIZE; do

@@ -18,7 +18,7 @@ DEV = "cuda"
 N_IMG = 16
 
 
-DEFAULTS = {"7": 1, "8": 1, "14": 1, "16": 1, "20": 1, "21": 1}  # sdmoe_tune knobs whose default is not 0
+DEFAULTS = {"7": 1, "8": 1, "14": 1, "16": 1, "20": 1, "21": 1, "23": 1}  # sdmoe_tune knobs whose default is not 0
 
 
 def rnd(*shape, scale=1.0):
@@ -134,7 +134,10 @@ def main():
     ap.add_argument("family")
     ap.add_argument("--tune", action="append", default=[])
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--nimg", type=int, default=16, help="images per launch (2 = one prompt with CFG)")
     a = ap.parse_args()
+    global N_IMG
+    N_IMG = a.nimg
     lib = _lib.load()
     fam = {"gn": gn_cases, "linear": linear_cases, "geglu": geglu_cases, "conv": conv_cases, "attn": attn_cases,
            "topk": topk_cases}
