@@ -28,7 +28,6 @@ constexpr int BK = 64;
 // tuning knobs (sdmoe_tune): 0 = LDS stages (0 = auto, 2 or 3); 1 = forced tile config (0 = auto)
 int g_stages = 0;
 int g_tile = 0;
-int g_bk = 0;
 int g_res16 = 1;  // knob 8: 1 = residual epilogues on the fp16 staging path (residual added in the copy-out), 0 = fp32
 int g_ksplit = 0;  // knob 9: forced split-K factor (0 = auto; 1 = never split), for tile sweeps
 int g_mfast = 1;   // knob 14: split-K conv grids ordered M-tile fastest (1) or split fastest (0)
@@ -1937,7 +1936,6 @@ extern "C" int sdmoe_tune(int knob, int value) {
   if (knob == 1 && value >= 0 && value <= 8) { g_tile = value; return SDMOE_OK; }
   if (knob == 9 && value >= 0 && value <= 32) { g_ksplit = value; return SDMOE_OK; }
   if (knob == 14 && (value == 0 || value == 1)) { g_mfast = value; return SDMOE_OK; }
-  if (knob == 2 && (value == 0 || value == 32 || value == 64)) { g_bk = value; return SDMOE_OK; }
   if (knob == 6 && value >= 0 && value <= 63) { g_diag = value; return SDMOE_OK; }
   if (knob == 8 && (value == 0 || value == 1)) { g_res16 = value; return SDMOE_OK; }
   if (knob == 15 && (value == 0 || value == 1 || value == 4)) { g_topk_tpw = value; return SDMOE_OK; }

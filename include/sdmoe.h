@@ -349,8 +349,7 @@ int sdmoe_cfg_multistep_step(const void* eps, long lde, float* lat, int B, int H
    (0 auto, 1 = 128x160, 2 = 64x160, 3 = 256x320 8-wave, 4 = 256x160 8-wave, 5 = 256x320 4x2-wave, 6 = 128x320 8-wave,
    7 = 128x160 8-wave, 8 = 64x320 8-wave; 7/8 plain GEMM / conv / LN-folded GEMM only); knob 9 = forced split-K
    factor (0 auto, 1 = never split, 2..32; halo convs: at most one 32-channel slice per split); knob 14 = split-K conv tile order: 1 (default) M-tile fastest (one XCD's
-   workgroups share weight slices in its L2), 0 split fastest; knob 2 = K-step
-   depth (0 auto, 32, 64); knob 4 = attention kernel (0 auto by shape,
+   workgroups share weight slices in its L2), 0 split fastest; knob 4 = attention kernel (0 auto by shape,
    1 = 32x32x16 MFMA kernel, 2 / 4 = 4-wave 16x16x32 kernel with 32 / 64 queries per wave, 64 for head_dim <= 40
    only; 8 = 16x16x32 kernel in 8-wave workgroups (head_dim <= 80));
    knob 6 = GEMM diagnostics bits (1 no K-loop loads, 2 no MFMA, 4 no epilogue, 8 no global stores);

@@ -32,17 +32,15 @@ def main():
     ap.add_argument("--stages", type=int, default=0)
     ap.add_argument("--tile", type=int, default=0, help="forced GEMM tile (sdmoe_tune knob 1), 0 = auto")
     ap.add_argument("--only", default="", help="run only rows whose label contains this")
-    ap.add_argument("--bk", type=int, default=0, help="GEMM K-step depth (sdmoe_tune knob 2), 0 = auto")
     ap.add_argument("--nqf", type=int, default=0, help="attention kernel (knob 4): 0 = auto, 1 = 32x32x16, 2/4 = 16x16x32 NQF")
     ap.add_argument("--diag", type=int, default=0, help="GEMM diagnostics (knob 6, bits): 1 = no K-loop loads, 2 = no MFMA, 4 = no epilogue")
     a = ap.parse_args()
     from sdmoe import _lib
     _lib.check(_lib.load().sdmoe_tune(0, a.stages), "tune")
     _lib.check(_lib.load().sdmoe_tune(1, a.tile), "tune")
-    _lib.check(_lib.load().sdmoe_tune(2, a.bk), "tune")
     _lib.check(_lib.load().sdmoe_tune(4, a.nqf), "tune")
     _lib.check(_lib.load().sdmoe_tune(6, a.diag), "tune")
-    print("stages", a.stages, "tile", a.tile, "bk", a.bk)
+    print("stages", a.stages, "tile", a.tile)
     n = a.nimg
     dev = "cuda"
     rows = []

@@ -74,7 +74,8 @@ def geglu_cases():
 
 def conv_cases():
     out = []
-    for H, Cin, Cout in [(64, 320, 320), (32, 640, 640), (16, 1280, 1280), (8, 1280, 1280), (32, 1280, 640)]:
+    for H, Cin, Cout in [(64, 320, 320), (64, 640, 320), (32, 640, 640), (32, 1280, 640), (32, 1920, 640), (32, 960, 640),
+                         (16, 1280, 1280), (8, 1280, 1280), (8, 2560, 1280)]:
         x = rnd(N_IMG * H * H, Cin)
         w = ops.conv_weight(rnd(Cout, 3, 3, Cin, scale=(9 * Cin) ** -0.5))
         out.append((f"conv {H}x{H} {Cin}->{Cout}", lambda x=x, w=w, H=H: ops.conv3x3(x, N_IMG, H, H, w),
