@@ -35,7 +35,6 @@ int g_mfast = 1;   // knob 14: split-K conv grids ordered M-tile fastest (1) or 
 // there is no residual (LN-folded projections 4-12 %, plain K = 320 linears ~3 % faster; with a residual its 16-B
 // residual loads measured 3-7 % slower than the staged copy-out), 2 = always, 0 = never
 int g_epi_direct = 1;
-int g_geglu_pp = 0;  // knob 25: routed GEGLU (ReLU / SiLU / erf GELU) on the ping-pong kernel, geglu_pp.hip
 int g_diag = 0;  // knob 6, diagnostics only (results garbage): bit 0 = no K-loop operand loads, bit 1 = no MFMAs,
                  // bit 4 = no A-operand pieces, bit 5 = no B-operand pieces,
                  // bit 2 = no epilogue (nothing stored), bit 3 = epilogue without its global stores
@@ -1749,11 +1748,6 @@ extern "C" int sdmoe_linear_keep(const void* A, long lda, const void* keep, cons
                              workspace_floats, stream);
 }
 
-// the persistent ping-pong routed GEGLU (geglu_pp.hip)
-int geglu_pp_launch(const void* A, long lda, const void* W, long ldw, const void* bias, void* P, long ldp, int M,
-                    int F, int K, int act, void* score, long ld_score, int esize, int a_bytes, int w_bytes,
-                    hipStream_t s);
-
 extern "C" int sdmoe_linear_geglu(const void* A, long lda, const void* W, long ldw, const void* bias, void* P,
                                   long ldp, int M, int F, int K, int act, void* score, long ld_score, int esize,
                                   void* stream) {
@@ -1772,12 +1766,6 @@ extern "C" int sdmoe_linear_geglu(const void* A, long lda, const void* W, long l
   if (ab >= (long)OOB || wb >= (long)OOB) return SDMOE_ESHAPE;
   p.a_bytes = (int)ab; p.w_bytes = (int)wb;
   if (p.gelu_tab) return dispatch_geglu<MODE_GEGLU_GT>(p, (hipStream_t)stream);
-  // knob 25: the persistent ping-pong kernel (geglu_pp.hip) on the grids MODE_GEGLU runs on 256x320 tiles
-  if (g_geglu_pp && !g_tile && ((M + 255) / 256) * (2 * F / 320) >= 240) {
-    const int st = geglu_pp_launch(A, lda, W, ldw, bias, P, ldp, M, F, K, act, score, ld_score, esize, p.a_bytes,
-                                   p.w_bytes, (hipStream_t)stream);
-    if (st != SDMOE_EUNSUP) return st;
-  }
   return dispatch_geglu<MODE_GEGLU>(p, (hipStream_t)stream);
 }
 
@@ -1955,6 +1943,5 @@ extern "C" int sdmoe_tune(int knob, int value) {
   if (knob == 20 && (value == 0 || value == 1)) { g_gt320 = value; return SDMOE_OK; }
   if (knob == 21 && (value == 0 || value == 1)) { g_narrow = value; return SDMOE_OK; }
   if (knob == 23 && value >= 0 && value <= 2) { g_epi_direct = value; return SDMOE_OK; }
-  if (knob == 25 && (value == 0 || value == 1)) { g_geglu_pp = value; return SDMOE_OK; }
   return SDMOE_EARG;
 }
