@@ -1480,8 +1480,10 @@ int dispatch(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
   if constexpr (MODE == MODE_CONV) {
     // 8x8-level 3x3 convs (M = 1024, K = 9 x 1280 / 9 x 2560): 8-wave 128x160 tiles (wave tile 32x80), 2-stage ring
     // (two workgroups per CU), 8-way split-K: 44.6 / 68.2 us vs 51.2 / 72.8 on 256x160 4x2 waves (tile_sweep.py)
+    // At one prompt per call (M = 128: 8 tiles) the fixed 8-way split left 64 workgroups streaming ~23 K-steps each
+    // behind a 2-stage ring; such grids (<= 16 tiles) take launch_tile's latency-regime split instead (16-24 ways)
     if (p.stride == 1 && p.N % 160 == 0 && p.M <= 1024 && p.K >= 9 * 1280)
-      return launch_tile<128, 160, 4, 2, MODE>(p, ws, ws_floats, s, 8, 2);
+      return launch_tile<128, 160, 4, 2, MODE>(p, ws, ws_floats, s, nt160_128 <= 16 ? 0 : 8, 2);
     if (p.stride == 1 && p.N % 320 == 0 && nt320 < 240 && p.K >= 9 * 1280 && p.M >= 2048 && p.M <= 4096)
       return launch_tile<256, 320, 2, 4, MODE>(p, ws, ws_floats, s);
     if (p.stride == 2 && p.N % 160 == 0 && p.M >= 8192) return launch_tile<64, 160, 2, 2, MODE>(p, ws, ws_floats, s);
@@ -1490,7 +1492,9 @@ int dispatch(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
     // 78.4-80.1 us with the auto ~one-per-CU split of 2, on every tile shape (same box)
     if (p.stride == 2 && p.N % 160 == 0 && p.M < 8192) {
       if (p.M > 2048) return launch_tile<128, 160, 2, 2, MODE>(p, ws, ws_floats, s, 4);
-      return launch_tile<64, 160, 2, 2, MODE>(p, ws, ws_floats, s, 4);
+      // (<= 16 tiles, the 16x16 -> 8x8 downsampler at one prompt: launch_tile's latency-regime split)
+      const int nt64 = ((p.M + 63) / 64) * (p.N / 160);
+      return launch_tile<64, 160, 2, 2, MODE>(p, ws, ws_floats, s, nt64 <= 16 ? 0 : 4);
     }
   }
   if (p.N % 160 == 0 && p.K >= 2560 && nt160_128 < 300 && !(MODE == MODE_CONV && p.stride == 2))
