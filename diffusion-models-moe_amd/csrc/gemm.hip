@@ -35,6 +35,7 @@ int g_mfast = 1;   // knob 14: split-K conv grids ordered M-tile fastest (1) or 
 // there is no residual (LN-folded projections 4-12 %, plain K = 320 linears ~3 % faster; with a residual its 16-B
 // residual loads measured 3-7 % slower than the staged copy-out), 2 = always, 0 = never
 int g_epi_direct = 1;
+int g_cus = 256;  // compute units of the device (set on the first launch from hipDeviceAttributeMultiprocessorCount)
 int g_diag = 0;  // knob 6, diagnostics only (results garbage): bit 0 = no K-loop operand loads, bit 1 = no MFMAs,
                  // bit 4 = no A-operand pieces, bit 5 = no B-operand pieces,
                  // bit 2 = no epilogue (nothing stored), bit 3 = epilogue without its global stores
@@ -1330,6 +1331,14 @@ int g_halo = 1;
 // the tile grid is under ~one wave of CUs
 template <int BM, int MODE>
 int launch_halo(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
+  static const bool cus_init = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) ==
+        hipSuccess && n > 0)
+      g_cus = n;
+    return true;
+  }();
+  (void)cus_init;
   constexpr int HW_ = halo_w(MODE);
   const int ntiles = (p.M / BM) * (p.N / 320);
   const int nsl = p.Cin / 32;
@@ -1344,6 +1353,9 @@ int launch_halo(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
     ksplit = (512 + ntiles - 1) / ntiles;
     if (ksplit > 32) ksplit = 32;
     if (ksplit > nsl / 2) ksplit = nsl / 2;
+    // whole rounds of one 8-wave workgroup per CU: 16 tiles x 20 splits left 64 workgroups alone in a second
+    // round (8 -> 16 upsample at one prompt: 43.2 vs 30.9 us with 16 splits, profiles/r05_b1_conv_split_sweep.txt)
+    if (ntiles * ksplit > g_cus && ntiles <= g_cus) ksplit = (g_cus / ntiles) * ((ksplit * ntiles) / g_cus);
     while (ksplit > 1 && (long)ksplit * p.M * p.N * 4 > (96L << 20)) --ksplit;
     while (ksplit > 1 && (long)ksplit * p.M * p.N > ws_floats) --ksplit;
     if (ksplit < 1) ksplit = 1;

@@ -80,6 +80,11 @@ def conv_cases():
         w = ops.conv_weight(rnd(Cout, 3, 3, Cin, scale=(9 * Cin) ** -0.5))
         out.append((f"conv {H}x{H} {Cin}->{Cout}", lambda x=x, w=w, H=H: ops.conv3x3(x, N_IMG, H, H, w),
                     2 * N_IMG * H * H * Cout * 9 * Cin, "F"))
+    for H, C in [(32, 640), (16, 1280), (8, 1280)]:  # the nearest-2x upsample convs (input H x H)
+        x = rnd(N_IMG * H * H, C)
+        w = ops.conv_weight(rnd(C, 3, 3, C, scale=(9 * C) ** -0.5))
+        out.append((f"conv up {H}->{2 * H} {C}->{C}", lambda x=x, w=w, H=H: ops.conv3x3(x, N_IMG, H, H, w, upsample=True),
+                    2 * N_IMG * 4 * H * H * C * 9 * C, "F"))
     return out
 
 
