@@ -1,7 +1,7 @@
 """Per-launch device time of U-Net ops at the bench's shapes (16 images), under one or more sdmoe_tune settings.
 
 usage: python tools/micro_ab.py FAMILY [--tune "k=v,k=v"]... [--iters 50]
-FAMILY: gn | linear | geglu | conv | attn | topk | all. Each case is launched back to back `iters` times between two HIP events on
+FAMILY: gn | linear | geglu | keep | conv | attn | topk | all. Each case is launched back to back `iters` times between two HIP events on
 the launch stream (warm L2: a relative A/B tool, not the pipeline's cold-cache numbers: tools/op_breakdown.py)."""
 import argparse
 import os
@@ -69,6 +69,20 @@ def geglu_cases():
                     2 * M * 2 * F * C, "F"))
         fold = ops.LNFold(rnd(3 * C, C, scale=C ** -0.5), rnd(C) * 0.1 + 1, rnd(C) * 0.1, 1e-5)
         out.append((f"linear_ln M={M} N={3 * C} K={C}", lambda x=x, f=fold: ops.linear_ln(x, f), 2 * M * 3 * C * C, "F"))
+    return out
+
+
+def keep_cases():
+    """The routed FFN down projection (keep-masked A operand, + residual) at each U-Net level (20 % of neurons kept)."""
+    out = []
+    for M, C in [(N_IMG * 4096, 320), (N_IMG * 1024, 640), (N_IMG * 256, 1280)]:
+        F = 4 * C
+        x, w, bias, r = rnd(M, F), rnd(C, F, scale=F ** -0.5), rnd(C, scale=0.1), rnd(M, C)
+        g = torch.Generator(device="cpu").manual_seed(M + C)
+        keep = torch.randint(0, 2 ** 62, (F // 64, M), generator=g, dtype=torch.int64).to(DEV)
+        y = torch.empty(M, C, device=DEV, dtype=torch.float16)
+        out.append((f"keep M={M} N={C} K={F} +res", lambda x=x, keep=keep, w=w, bias=bias, r=r, y=y:
+                    ops.linear_keep(x, keep, w, bias, residual=r, out=y), 2 * M * C * F, "F"))
     return out
 
 
@@ -146,7 +160,7 @@ def main():
     N_IMG = a.nimg
     lib = _lib.load()
     fam = {"gn": gn_cases, "linear": linear_cases, "geglu": geglu_cases, "conv": conv_cases, "attn": attn_cases,
-           "topk": topk_cases}
+           "topk": topk_cases, "keep": keep_cases}
     cases = [c for k in (fam if a.family == "all" else [a.family]) for c in fam[k]()]
     settings = a.tune or [""]
     table = {}
