@@ -1407,6 +1407,10 @@ int try_halo(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
   if (p.Wd == 64 && hw % 256 == 0) return launch_halo<256, MODE_CONVH64>(p, ws, ws_floats, s);
   // 16-wide outputs: a whole 16x16 image per 256-row tile, K split over slices (1280 -> 1280: 127.6 vs 133.0 us)
   if (g_halo != 2 && p.Wd == 16 && hw % 256 == 0) return launch_halo<256, MODE_CONVH16>(p, ws, ws_floats, s);
+  // 32-wide outputs: halo tiles (8 output rows) for the wide-input convs only (up-block conv1, Cin 1920 / 1280): 292 vs
+  // 307 us and 206 vs 208 at 16 images, 62 vs 66 and 52 vs 54 at 2; at Cin 640 / 960 they ran 10-14 % slower
+  // (profiles/r05_halo32_geglu_diag.txt)
+  if (g_halo == 1 && p.Wd == 32 && hw % 256 == 0 && p.Cin >= 1280) return launch_halo<256, MODE_CONVH32>(p, ws, ws_floats, s);
   if (g_halo == 3 && p.Wd == 32 && hw % 256 == 0) return launch_halo<256, MODE_CONVH32>(p, ws, ws_floats, s);
   if (g_halo < 2) return -1;
   if (p.Wd == 32 && hw % 128 == 0) return launch_halo<128, MODE_CONVH32>(p, ws, ws_floats, s);
