@@ -1322,9 +1322,9 @@ int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s, int ks_w
 
 // knob 16: halo-tiled stride-1 3x3 convs: 1 (default) = where they measured faster than the shifted-tile kernel:
 // 64-wide outputs (256-row tiles), 16-wide ones on 256-row tiles (a whole image), the 32 -> 64, 16 -> 32 (256-row
-// tiles) and 8 -> 16 upsample convs; 2 = every 128-row tile instead (32- / 16-wide outputs: 5-17 % slower, their
-// 32-deep K-steps carry half the MFMAs per barrier); 3 = the default plus 32-wide outputs on 256-row tiles (135.1 vs
-// 118.0 us at 640 -> 640: not kept); 0 = off
+// tiles) and 8 -> 16 upsample convs, 32-wide outputs with Cin >= 1280 (256-row tiles); 2 = every 128-row tile instead
+// (32- / 16-wide outputs: 5-17 % slower, their 32-deep K-steps carry half the MFMAs per barrier); 3 = the default plus
+// every 32-wide output on 256-row tiles (135.1 vs 118.0 us at 640 -> 640); 0 = off
 int g_halo = 1;
 
 // halo conv launch: BM x 320 tiles (8 waves 2 x 4, BK 32, 3-stage B ring), K split over whole 32-channel slices when
