@@ -1404,6 +1404,11 @@ int try_halo(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
     return -1;
   }
   const int hw = p.H * p.Wd;
+  // 64-wide outputs at one prompt (<= 32 tiles of 256 rows): 128-row tiles (two output rows), twice the workgroups
+  // for the split to fill the chip with: 33.6 vs 41.0 us (320 -> 320) and 43.5 vs 51.1 (640 -> 320) at 2 images,
+  // --batch 1 +0.8 % (profiles/r05_halo64_b1.txt)
+  if (g_halo == 1 && p.Wd == 64 && hw % 128 == 0 && (p.M / 256) * (p.N / 320) <= 32)
+    return launch_halo<128, MODE_CONVH64>(p, ws, ws_floats, s);
   if (p.Wd == 64 && hw % 256 == 0) return launch_halo<256, MODE_CONVH64>(p, ws, ws_floats, s);
   // 16-wide outputs: a whole 16x16 image per 256-row tile, K split over slices (1280 -> 1280: 127.6 vs 133.0 us)
   if (g_halo != 2 && p.Wd == 16 && hw % 256 == 0) return launch_halo<256, MODE_CONVH16>(p, ws, ws_floats, s);

@@ -428,7 +428,8 @@ def test_conv3x3_halo_tiles(H, Cin, Cout, nimg, up):
     wc = ops.conv_weight(w)
     outs = []
     kw = {} if up else dict(coladd=temb, coladd_bstride=Cout, residual=res)
-    # 1 default; 2: the 128-row halo tiles the default leaves off; 3: 32-wide outputs on 256-row tiles; 0: shifted
+    # 1 default (64-wide at <= 32 tiles: 128-row tiles); 2: the 128-row halo tiles the default leaves off; 3: 32-wide
+    # outputs on 256-row tiles; 0: shifted
     for halo in (1, 2, 3, 0):
         _with_tune([(16, halo)], lambda: outs.append(ops.conv3x3(x, nimg, H, H, wc, b, upsample=up, **kw)))
     for o in outs:
