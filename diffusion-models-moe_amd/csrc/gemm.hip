@@ -1397,6 +1397,9 @@ int try_halo(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
     const int ohw = 4 * p.H * p.Wd;
     if (p.Wd == 32 && ohw % 256 == 0) return launch_halo<256, MODE_CONVHUP64>(p, ws, ws_floats, s);
     if (p.Wd == 8 && ohw % 128 == 0) return launch_halo<128, MODE_CONVHUP16>(p, ws, ws_floats, s);  // 125.6 vs 137.0
+    // one prompt per call (<= 32 tiles of 256 output rows): 128-row tiles, 68.8 vs 72.5 us at 2 images
+    if (g_halo == 1 && p.Wd == 16 && ohw % 128 == 0 && (p.M / 256) * (p.N / 320) <= 32)
+      return launch_halo<128, MODE_CONVHUP32>(p, ws, ws_floats, s);
     // 16 -> 32 upsample on 256-row tiles (8 output rows, K split over slices): 360.3 vs 383.1-395.8 us
     if (g_halo != 2 && p.Wd == 16 && ohw % 256 == 0) return launch_halo<256, MODE_CONVHUP32>(p, ws, ws_floats, s);
     if (g_halo < 2) return -1;
@@ -1410,6 +1413,14 @@ int try_halo(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
   if (g_halo == 1 && p.Wd == 64 && hw % 128 == 0 && (p.M / 256) * (p.N / 320) <= 32)
     return launch_halo<128, MODE_CONVH64>(p, ws, ws_floats, s);
   if (p.Wd == 64 && hw % 256 == 0) return launch_halo<256, MODE_CONVH64>(p, ws, ws_floats, s);
+  // one prompt per call (<= 32 tiles of 256 rows): 128-row tiles for the 16-wide and the narrow-input 32-wide convs,
+  // twice the workgroups for the split -- 31.9 vs 39.9 us (16x16 1280 -> 1280), 32.3 vs 35.2 (32x32 640 -> 640), 38.9
+  // vs 41.3 (960 -> 640) at 2 images; the Cin >= 1280 32-wide convs keep 256-row tiles (57.8 vs 52.0 us)
+  // (profiles/r05_halo128_b1.txt)
+  const bool small = (p.M / 256) * (p.N / 320) <= 32;
+  if (g_halo == 1 && small && p.Wd == 16 && hw % 128 == 0) return launch_halo<128, MODE_CONVH16>(p, ws, ws_floats, s);
+  if (g_halo == 1 && small && p.Wd == 32 && hw % 128 == 0 && p.Cin < 1280)
+    return launch_halo<128, MODE_CONVH32>(p, ws, ws_floats, s);
   // 16-wide outputs: a whole 16x16 image per 256-row tile, K split over slices (1280 -> 1280: 127.6 vs 133.0 us)
   if (g_halo != 2 && p.Wd == 16 && hw % 256 == 0) return launch_halo<256, MODE_CONVH16>(p, ws, ws_floats, s);
   // 32-wide outputs: halo tiles (8 output rows) for the wide-input convs only (up-block conv1, Cin 1920 / 1280): 292 vs
