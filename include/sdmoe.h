@@ -360,8 +360,9 @@ int sdmoe_cfg_multistep_step(const void* eps, long lde, float* lat, int B, int H
    knob 15 = top-k expert selection kernels: 0 (default) one token per wave at M <= 16384, four above, and the keep
    bits at E <= 64 with one quad of lanes per token; 1 / 4 = always the ballot kernel at one / four tokens per wave;
    knob 16 = halo-tiled 3x3 convs: 1 (default) where measured faster (64- and 16-wide outputs, the upsample convs,
-   32-wide outputs with Cin >= 1280), 2 = every 128-row halo tile instead, 3 = the default plus every 32-wide output
-   on 256-row tiles, 0 = off;
+   32-wide outputs with Cin >= 1280; grids of <= 32 256-row tiles -- one prompt per call -- on 128-row tiles for the
+   64-, 16- and narrow-input 32-wide outputs and the 16 -> 32 upsample), 2 = every 128-row halo tile instead, 3 = the
+   default plus every 32-wide output on 256-row tiles, 0 = off;
    knob 20 = table-GELU routed GEGLU tiles: 1 (default) 256x320 like the ReLU kernel, 0 = 256x160 (4x2 waves);
    knob 21 = convs with at most 32 output channels (conv_out): 1 (default) 128x32 tiles, 0 = 128x64;
    knob 23 = fp16 GEMM / conv epilogues: 1 (default) 16-B row pieces stored straight from the MFMA fragments (two
