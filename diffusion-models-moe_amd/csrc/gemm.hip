@@ -1539,7 +1539,9 @@ int dispatch(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
     if (p.N <= 32 && g_narrow) return launch_tile<128, 32, 2, 2, MODE>(p, ws, ws_floats, s);
   if (p.N <= 64) return launch_tile<128, 64, 2, 2, MODE>(p, ws, ws_floats, s);
   if (p.N % 160 == 0) {
-    if (nt160_128 >= 200 || p.M > 2048) return launch_tile<128, 160, 2, 2, MODE>(p, ws, ws_floats, s);
+    // plain GEMMs under ~one wave of 128x160 tiles take 64x160 at any M: the 64x64 level's K = 320 projections at one
+    // prompt (M = 8192, N = 320: 128 tiles) 7.8 vs 10.6 us, 8.4 vs 11.8 with the residual (r05_b1_linear_tiles.txt)
+    if (nt160_128 >= 200 || (p.M > 2048 && MODE != MODE_GEMM)) return launch_tile<128, 160, 2, 2, MODE>(p, ws, ws_floats, s);
     return launch_tile<64, 160, 2, 2, MODE>(p, ws, ws_floats, s);
   }
   const int nt128 = ((p.M + 127) / 128) * ((p.N + 127) / 128);

@@ -39,7 +39,7 @@ def rnd(*shape, scale=1.0, dtype=torch.float16, seed=0):
 
 
 @pytest.mark.parametrize("M,N,K", [(256, 320, 320), (130, 640, 768), (4096, 2560, 320), (64, 1280, 5120),
-                                   (1, 1280, 320), (1000, 960, 320), (77, 1280, 768)])
+                                   (1, 1280, 320), (1000, 960, 320), (77, 1280, 768), (8192, 320, 320)])
 def test_linear_bias_residual(M, N, K):
     x = rnd(M, K, seed=1)
     w = rnd(N, K, scale=K ** -0.5, seed=2)

@@ -45,6 +45,7 @@ def linear_cases():
     for M, N, K, res in [(65536, 320, 320, True), (65536, 320, 320, False), (16384, 640, 640, True),
                          (16384, 640, 640, False), (4096, 1280, 1280, True), (4096, 1280, 1280, False),
                          (65536, 960, 320, False), (1024, 1280, 1280, True)]:
+        M = M * N_IMG // 16  # the bench's rows at 16 images; --nimg 2 gives the one-prompt shapes
         x, w, bias = rnd(M, K), rnd(N, K, scale=K ** -0.5), rnd(N, scale=0.1)
         r = rnd(M, N) if res else None
         y = torch.empty(M, N, device=DEV, dtype=torch.float16)
