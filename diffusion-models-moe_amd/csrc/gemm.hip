@@ -1460,6 +1460,10 @@ int dispatch_geglu(const GemmParams& p, hipStream_t s) {
     if (g_tile == 5) return launch_tile<256, 320, 4, 2, MODE>(p, nullptr, 0, s);
     return launch_tile<256, 320, 2, 4, MODE>(p, nullptr, 0, s);
   }
+  // one prompt per call at the 16x16 level (M = 512, N = 10240): 8-wave 128x160 tiles, 20.5 vs 27.3 us on the 4-wave
+  // ones (the 32x32 level's M = 2048 measured 24.3 vs 19.0 with them; profiles/r05_b1_geglu_keep_tiles.txt)
+  if constexpr (MODE != MODE_GEGLU_GT)
+    if (p.M <= 1024 && nt160_128 >= 128) return launch_tile<128, 160, 4, 2, MODE>(p, nullptr, 0, s);
   if (nt160_128 >= 200 || p.M > 2048) return launch_tile<128, 160, 2, 2, MODE>(p, nullptr, 0, s);
   return launch_tile<64, 160, 2, 2, MODE>(p, nullptr, 0, s);
 }
@@ -1529,6 +1533,10 @@ int dispatch(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
       return launch_tile<64, 160, 2, 2, MODE>(p, ws, ws_floats, s, nt64 <= 16 ? 0 : 4);
     }
   }
+  // the keep-masked down projection at one prompt (<= 128 tiles of 128x160): 64x160 tiles -- 22.3 vs 29.5 us at the
+  // 64x64 level, 27.5 vs 30.1 at 16x16 (profiles/r05_b1_geglu_keep_tiles.txt)
+  if constexpr (mode_akeep(MODE))
+    if (p.N % 160 == 0 && nt160_128 <= 128) return launch_tile<64, 160, 2, 2, MODE>(p, ws, ws_floats, s);
   if (p.N % 160 == 0 && p.K >= 2560 && nt160_128 < 300 && !(MODE == MODE_CONV && p.stride == 2))
     return launch_tile<256, 160, 4, 2, MODE>(p, ws, ws_floats, s);
   if (MODE == MODE_CONV_UP) {

@@ -58,6 +58,7 @@ def geglu_cases():
     """The fused routed GEGLU projection (relu, expert 20, top-k 0.2) and the LN-folded QKV at each U-Net level."""
     out = []
     for M, C in [(65536, 320), (16384, 640), (4096, 1280)]:
+        M = M * N_IMG // 16
         F, E = 4 * C, 4 * C // 20
         x = rnd(M, C)
         w = rnd(2 * F, C, scale=C ** -0.5)
