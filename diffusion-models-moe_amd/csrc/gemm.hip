@@ -1534,9 +1534,11 @@ int dispatch(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
     }
   }
   // the keep-masked down projection at one prompt (<= 128 tiles of 128x160): 64x160 tiles -- 22.3 vs 29.5 us at the
-  // 64x64 level, 27.5 vs 30.1 at 16x16 (profiles/r05_b1_geglu_keep_tiles.txt)
+  // 64x64 level (profiles/r05_b1_geglu_keep_tiles.txt). Only below K = 2560: there the plain GEMM of the same shape
+  // takes the same 64x160 tile and split, so keep-masked and masked-then-plain stay bit-identical; at K >= 2560 both
+  // take the 256x160 rule below.
   if constexpr (mode_akeep(MODE))
-    if (p.N % 160 == 0 && nt160_128 <= 128) return launch_tile<64, 160, 2, 2, MODE>(p, ws, ws_floats, s);
+    if (p.N % 160 == 0 && p.K < 2560 && nt160_128 <= 128) return launch_tile<64, 160, 2, 2, MODE>(p, ws, ws_floats, s);
   if (p.N % 160 == 0 && p.K >= 2560 && nt160_128 < 300 && !(MODE == MODE_CONV && p.stride == 2))
     return launch_tile<256, 160, 4, 2, MODE>(p, ws, ws_floats, s);
   if (MODE == MODE_CONV_UP) {
