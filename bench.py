@@ -69,8 +69,10 @@ def parse():
                    help="cpu_baseline: time one whole image (all inference steps of the oracle's DDIM+CFG loop, "
                         "several minutes) instead of the bounded cpu-evals sample")
     p.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)
-    p.add_argument("--traffic", type=str, default=os.path.join(ROOT, "profiles", "pmc_conv_traffic.json"),
-                   help="PMC summary json from tools/pmc_traffic.py (HBM bytes per conv launch)")
+    p.add_argument("--traffic", type=str, default=None,
+                   help="PMC summary json from tools/pmc_traffic.py (HBM bytes per conv launch); default "
+                        "profiles/pmc_conv_traffic.json (8 prompts/GPU) or profiles/pmc_conv_traffic_b<B>.json; used "
+                        "only when its recorded model / prompts per GPU / mask are this run's")
     return p.parse_args()
 
 
@@ -355,6 +357,9 @@ def main():
         return launch_probe(args)
     if args.batch is None:
         args.batch = 2 if args.model == "sdxl" else 8
+    if args.traffic is None:
+        args.traffic = os.path.join(ROOT, "profiles", "pmc_conv_traffic" + ("" if args.batch == 8 else
+                                                                            f"_b{args.batch}") + ".json")
     if args.act is None:
         args.act = "gelu" if args.model == "sdxl" else "relu"
     world, rank, local = setup_dist(args.gpus)
@@ -437,13 +442,17 @@ def main():
         if n:
             achieved = flops / (ms / 1e3) / 1e12
             traffic, traffic_src = None, None
-            if args.traffic and os.path.exists(args.traffic) and args.model == "sd14":  # PMC file is the SD-1.4 run
-                pmc = json.load(open(args.traffic))
+            pmc = json.load(open(args.traffic)) if args.traffic and os.path.exists(args.traffic) else {}
+            # only a PMC run of THIS workload (model, prompts per GPU, mask) is evidence for this line's launches
+            if pmc and (pmc.get("model"), pmc.get("batch"), pmc.get("mask")) == (args.model, args.batch, args.mask):
                 traffic = pmc.get("bytes_per_launch")
                 # not measured in this process: the committed rocprofv3 --pmc passes (FETCH_SIZE x2, WRITE_SIZE) of
                 # this bench command on the build named in the file
                 traffic_src = (f"{os.path.relpath(args.traffic, ROOT)} (rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes"
                                f" of bench.py, build {pmc.get('build', '?')})")
+            elif pmc:
+                traffic_src = (f"null: {os.path.relpath(args.traffic, ROOT)} profiles model {pmc.get('model')}, "
+                               f"{pmc.get('batch')} prompts/GPU, mask {pmc.get('mask')} -- not this run's launches")
             roof = {"bound": "mfma", "kernel": "sdmoe_conv3x3 / _sc / _gn: implicit-GEMM conv (gemm_kernel MODE 1/2 "
                                                "shifted tiles, MODE 9/11/12/14 halo tiles, + split-K reduce where used)",
                     "achieved": round(achieved, 1), "peak": PEAK_FP16_TFLOPS, "unit": "TFLOP/s",

@@ -35,7 +35,8 @@ int g_mfast = 1;   // knob 14: split-K conv grids ordered M-tile fastest (1) or 
 // there is no residual (LN-folded projections 4-12 %, plain K = 320 linears ~3 % faster; with a residual its 16-B
 // residual loads measured 3-7 % slower than the staged copy-out), 2 = always, 0 = never
 int g_epi_direct = 1;
-int g_cus = 256;  // compute units of the device (set on the first launch from hipDeviceAttributeMultiprocessorCount)
+int g_cus = 256;  // compute units of the device (device_cus(): hipDeviceAttributeMultiprocessorCount, queried once)
+bool g_cus_init = false;
 int g_diag = 0;  // knob 6, diagnostics only (results garbage): bit 0 = no K-loop operand loads, bit 1 = no MFMAs,
                  // bit 4 = no A-operand pieces, bit 5 = no B-operand pieces,
                  // bit 2 = no epilogue (nothing stored), bit 3 = epilogue without its global stores
@@ -1253,33 +1254,77 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
   }
 }
 
-template <int BM, int BN, int WMW, int WNW, int MODE>
-int launch_tile(GemmParams p, float* ws, long ws_floats, hipStream_t s, int ks_want = 0, int stages_want = 0) {
-  const int ntiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+// ---- launch planning (host only) ----------------------------------------------------------------------------
+// A launch = a tile instantiation + a split-K factor. The split (with the 64-deep K walk every tile shares) is the
+// only thing that decides each output's fp32 summation order -- tile shape and wave arrangement do not -- so it is
+// computed by ONE function (plan_split) from the chosen tile, and the masked modes (MODE_KEEP / WMASK / KEEPW) take
+// the plain GEMM's plan for their shape (dispatch below): a keep- or Wanda-masked product is bit-identical to masking
+// the operand first and running sdmoe_linear by construction, not by a restated copy of the plain rules.
+enum TileId { T128x160, T64x160, T256x320, T256x160_42, T256x320_42, T128x320, T128x160_42, T64x320, T128x32, T128x64,
+              T128x128, T64x128, NTILE };
+struct TileShape { int bm, bn, wmw, wnw; };
+constexpr TileShape kTile[NTILE] = {{128, 160, 2, 2}, {64, 160, 2, 2}, {256, 320, 2, 4}, {256, 160, 4, 2},
+                                    {256, 320, 4, 2}, {128, 320, 2, 4}, {128, 160, 4, 2}, {64, 320, 2, 4},
+                                    {128, 32, 2, 2},  {128, 64, 2, 2},  {128, 128, 2, 2}, {64, 128, 2, 2}};
+struct Plan {
+  int tile;
+  int ks_want;      // split-K wish of the tile rule (0 = the policy in plan_split)
+  int stages_want;  // LDS ring depth wish (0 = launch_tile's policy)
+};
+
+// compute units of the current device, queried once (both split policies size their grids by it; 256 on MI355X, and
+// the fallback when no device answers, e.g. sdmoe_gemm_plan on a CPU host). Splits -- hence the fp32 summation order
+// of split-K outputs -- are per-device-SKU by design.
+int device_cus() {
+  if (g_cus_init) return g_cus;
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) ==
+      hipSuccess && n > 0)
+    g_cus = n;
+  g_cus_init = true;
+  return g_cus;
+}
+
+// split-K factor of a launch on tile t (mode: the tile rule's MODE; ws: whether a slab workspace was handed in)
+int plan_split(const TileShape& t, int mode, const GemmParams& p, const float* ws, long ws_floats, int ks_want) {
+  const int ntiles = ((p.M + t.bm - 1) / t.bm) * ((p.N + t.bn - 1) / t.bn);
   const int nk = p.K / 64;
-  if (p.w_bstride && p.rows_per_batch % BM) return SDMOE_EUNSUP;  // a tile would straddle two images' weights
+  const int cus = device_cus();
   int ksplit = 1;
-  // fill the chip: split K when the tile grid covers well under one wave of 256 CUs
+  // fill the chip: split K when the tile grid covers well under one wave of CUs
   if (ws && (g_ksplit > 0 || ks_want > 0)) {
     ksplit = g_ksplit > 0 ? g_ksplit : ks_want;
     if (ksplit > nk) ksplit = nk;
     while (ksplit > 1 && (long)ksplit * p.M * p.N > ws_floats) --ksplit;
-  } else if (ws && (MODE == MODE_CONV || MODE == MODE_CONV_UP) && ntiles <= 16 && nk >= 64) {
+  } else if (ws && (mode == MODE_CONV || mode == MODE_CONV_UP) && ntiles <= 16 && nk >= 64) {
     // latency regime (one prompt per call, base_receiver.py:73: 8x8 / 16x16 / 32x32 convs at batch 2): up to two
     // workgroups per CU, >= 11 K-steps per split, <= 64 MB of fp32 slabs -- B = 1 sweep (profiles/r05_b1_split_sweep.txt):
     // 8x8 1280 -> 1280 28.1 -> 23.5 us, 2560 -> 1280 44.3 -> 29.6, 16x16 stride 2 39.9 -> 22.0, 32x32 1280 -> 640
     // 64.2 -> 55.2 (at most 8 splits before)
-    ksplit = (512 + ntiles - 1) / ntiles;
+    ksplit = (2 * cus + ntiles - 1) / ntiles;
     if (ksplit > 24) ksplit = 24;
     if (ksplit > nk / 11) ksplit = nk / 11;
     while (ksplit > 1 && (long)ksplit * p.M * p.N * 4 > (64L << 20)) --ksplit;
     while (ksplit > 1 && (long)ksplit * p.M * p.N > ws_floats) --ksplit;
-  } else if (ws && ntiles < 192 && nk >= 16) {
-    ksplit = (256 + ntiles - 1) / ntiles;
+  } else if (ws && ntiles < 3 * cus / 4 && nk >= 16) {
+    ksplit = (cus + ntiles - 1) / ntiles;
     if (ksplit > 8) ksplit = 8;
     if (ksplit > nk / 4) ksplit = nk / 4;
     while (ksplit > 1 && (long)ksplit * p.M * p.N > ws_floats) --ksplit;
   }
+  if (ksplit < 1) ksplit = 1;
+  // no empty trailing split: ceil(nk / ksplit) K-steps per split, as many splits as that takes (e.g. nk = 180 at 16
+  // wanted: 12 per split -> 15 splits, not a 16th that writes a zero slab the reduce then reads)
+  const int kchunk = (nk + ksplit - 1) / ksplit;
+  return (nk + kchunk - 1) / kchunk;
+}
+
+template <int BM, int BN, int WMW, int WNW, int MODE>
+int launch_tile(GemmParams p, float* ws, hipStream_t s, int ksplit, int stages_want = 0) {
+  const int ntiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+  const int nk = p.K / 64;
+  if (p.w_bstride && p.rows_per_batch % BM) return SDMOE_EUNSUP;  // a tile would straddle two images' weights
+  if (ksplit > 1 && !ws) return SDMOE_EARG;
   p.ksplit = ksplit > 1 ? ksplit : 1;
   constexpr int NTH = 64 * WMW * WNW;
   p.kchunk = (nk + p.ksplit - 1) / p.ksplit;
@@ -1331,14 +1376,7 @@ int g_halo = 1;
 // the tile grid is under ~one wave of CUs
 template <int BM, int MODE>
 int launch_halo(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
-  static const bool cus_init = [] {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) ==
-        hipSuccess && n > 0)
-      g_cus = n;
-    return true;
-  }();
-  (void)cus_init;
+  const int cus = device_cus();
   constexpr int HW_ = halo_w(MODE);
   const int ntiles = (p.M / BM) * (p.N / 320);
   const int nsl = p.Cin / 32;
@@ -1350,17 +1388,17 @@ int launch_halo(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
     // latency regime (batch 2: whole 16x16 images, the 8 -> 16 upsample, 64x64 at 32 tiles): up to two workgroups
     // per CU, >= 2 slices per split, <= 96 MB of fp32 slabs -- B = 1 sweep: 16x16 1280 -> 1280 56.1 -> 40.9 us
     // (20 splits), 2560 -> 1280 91.7 -> 55.3, 8 -> 16 upsample 38.0 -> 31.7 (at most 8 splits before)
-    ksplit = (512 + ntiles - 1) / ntiles;
+    ksplit = (2 * cus + ntiles - 1) / ntiles;
     if (ksplit > 32) ksplit = 32;
     if (ksplit > nsl / 2) ksplit = nsl / 2;
     // whole rounds of one 8-wave workgroup per CU: 16 tiles x 20 splits left 64 workgroups alone in a second
     // round (8 -> 16 upsample at one prompt: 43.2 vs 30.9 us with 16 splits, profiles/r05_b1_conv_split_sweep.txt)
-    if (ntiles * ksplit > g_cus && ntiles <= g_cus) ksplit = (g_cus / ntiles) * ((ksplit * ntiles) / g_cus);
+    if (ntiles * ksplit > cus && ntiles <= cus) ksplit = (cus / ntiles) * ((ksplit * ntiles) / cus);
     while (ksplit > 1 && (long)ksplit * p.M * p.N * 4 > (96L << 20)) --ksplit;
     while (ksplit > 1 && (long)ksplit * p.M * p.N > ws_floats) --ksplit;
     if (ksplit < 1) ksplit = 1;
   } else if (ws && ntiles < 200) {
-    ksplit = (256 + ntiles - 1) / ntiles;  // 6 / 8 splits: 172 vs 128 us at 16x16 x 1280 (r04)
+    ksplit = (cus + ntiles - 1) / ntiles;  // 6 / 8 splits: 172 vs 128 us at 16x16 x 1280 (r04)
     if (ksplit > 8) ksplit = 8;
     if (ksplit > nsl / 2) ksplit = nsl / 2;
     while (ksplit > 1 && (long)ksplit * p.M * p.N > ws_floats) --ksplit;
@@ -1446,50 +1484,48 @@ template <int MODE>
 int dispatch_geglu(const GemmParams& p, hipStream_t s) {
   const int nt320 = ((p.M + 255) / 256) * (p.N / 320);
   const int nt160_128 = ((p.M + 127) / 128) * (p.N / 160);
-  if (g_tile == 1) return launch_tile<128, 160, 2, 2, MODE>(p, nullptr, 0, s);
-  if (g_tile == 4) return launch_tile<256, 160, 4, 2, MODE>(p, nullptr, 0, s);
+  if (g_tile == 1) return launch_tile<128, 160, 2, 2, MODE>(p, nullptr, s, 1);
+  if (g_tile == 4) return launch_tile<256, 160, 4, 2, MODE>(p, nullptr, s, 1);
   if constexpr (MODE != MODE_GEGLU_GT)  // (no room for the GELU table behind that tile's staging)
-    if (g_tile == 7) return launch_tile<128, 160, 4, 2, MODE>(p, nullptr, 0, s);  // sweep: two workgroups per CU
+    if (g_tile == 7) return launch_tile<128, 160, 4, 2, MODE>(p, nullptr, s, 1);  // sweep: two workgroups per CU
   if (MODE == MODE_GEGLU_GT && g_tile == 0 && !g_gt320 && p.N % 320 == 0 && nt320 >= 240)
     // knob 20 = 0: the same rows on 256x160 tiles, 8 waves 4 x 2 (wave tile 64 x 80)
-    return launch_tile<256, 160, 4, 2, MODE>(p, nullptr, 0, s);
+    return launch_tile<256, 160, 4, 2, MODE>(p, nullptr, s, 1);
   if (p.N % 320 == 0 && nt320 >= 240) {
     // 2x4 waves (wave tile 128 rows x 40 neurons): with the row-fastest epilogue its 32-row staging passes are
     // conflict-free (4x2's 16-row passes are not: two 16-lane b128 groups mix column pairs); 174.6 vs 181.2 us at
     // M = 65536, 129.8 vs 132.9 at 16384, 103.4 vs 106.4 at 4096 (same box)
-    if (g_tile == 5) return launch_tile<256, 320, 4, 2, MODE>(p, nullptr, 0, s);
-    return launch_tile<256, 320, 2, 4, MODE>(p, nullptr, 0, s);
+    if (g_tile == 5) return launch_tile<256, 320, 4, 2, MODE>(p, nullptr, s, 1);
+    return launch_tile<256, 320, 2, 4, MODE>(p, nullptr, s, 1);
   }
   // one prompt per call at the 16x16 level (M = 512, N = 10240): 8-wave 128x160 tiles, 20.5 vs 27.3 us on the 4-wave
   // ones (the 32x32 level's M = 2048 measured 24.3 vs 19.0 with them; profiles/r05_b1_geglu_keep_tiles.txt)
   if constexpr (MODE != MODE_GEGLU_GT)
-    if (p.M <= 1024 && nt160_128 >= 128) return launch_tile<128, 160, 4, 2, MODE>(p, nullptr, 0, s);
-  if (nt160_128 >= 200 || p.M > 2048) return launch_tile<128, 160, 2, 2, MODE>(p, nullptr, 0, s);
-  return launch_tile<64, 160, 2, 2, MODE>(p, nullptr, 0, s);
+    if (p.M <= 1024 && nt160_128 >= 128) return launch_tile<128, 160, 4, 2, MODE>(p, nullptr, s, 1);
+  if (nt160_128 >= 200 || p.M > 2048) return launch_tile<128, 160, 2, 2, MODE>(p, nullptr, s, 1);
+  return launch_tile<64, 160, 2, 2, MODE>(p, nullptr, s, 1);
 }
 
+// Tile rule of the dense modes (GEMM, CONV, CONV_UP, GEMM_LN); the masked modes plan as MODE_GEMM (dispatch).
 template <int MODE>
-int dispatch(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
+Plan choose_tile(const GemmParams& p) {
+  static_assert(!mode_akeep(MODE) && !mode_wmask(MODE), "masked modes take the plain GEMM's plan");
   const int tm256 = (p.M + 255) / 256;
   // forced tile (sdmoe_tune knob 1): 1 = 128x160, 2 = 64x160, 3 = 256x320 (8 waves), 4 = 256x160 (8 waves)
-  if (g_tile == 1) return launch_tile<128, 160, 2, 2, MODE>(p, ws, ws_floats, s);
-  if (g_tile == 2) return launch_tile<64, 160, 2, 2, MODE>(p, ws, ws_floats, s);
-  if (g_tile == 3 && p.N % 320 == 0) return launch_tile<256, 320, 2, 4, MODE>(p, ws, ws_floats, s);
-  if (g_tile == 4 && p.N % 160 == 0) return launch_tile<256, 160, 4, 2, MODE>(p, ws, ws_floats, s);
-  if (g_tile == 5 && p.N % 320 == 0) return launch_tile<256, 320, 4, 2, MODE>(p, ws, ws_floats, s);
-  if (g_tile == 6 && p.N % 320 == 0) return launch_tile<128, 320, 2, 4, MODE>(p, ws, ws_floats, s);
+  if (g_tile == 1) return {T128x160, 0, 0};
+  if (g_tile == 2) return {T64x160, 0, 0};
+  if (g_tile == 3 && p.N % 320 == 0) return {T256x320, 0, 0};
+  if (g_tile == 4 && p.N % 160 == 0) return {T256x160_42, 0, 0};
+  if (g_tile == 5 && p.N % 320 == 0) return {T256x320_42, 0, 0};
+  if (g_tile == 6 && p.N % 320 == 0) return {T128x320, 0, 0};
   // sweep-only 8-wave tiles with a 32x80 wave tile (two workgroups per CU on a 2-stage ring)
-  if constexpr (MODE == MODE_GEMM || MODE == MODE_CONV || MODE == MODE_GEMM_LN) {
-    if (g_tile == 7 && p.N % 160 == 0) return launch_tile<128, 160, 4, 2, MODE>(p, ws, ws_floats, s);
-    if (g_tile == 8 && p.N % 320 == 0) return launch_tile<64, 320, 2, 4, MODE>(p, ws, ws_floats, s);
-  }
+  if (MODE != MODE_CONV_UP && g_tile == 7 && p.N % 160 == 0) return {T128x160_42, 0, 0};
+  if (MODE != MODE_CONV_UP && g_tile == 8 && p.N % 320 == 0) return {T64x320, 0, 0};
   // 8-wave 256x320 tile (wave tile 128x80: 2.5x the MFMA work per LDS byte of 64x80) whenever it alone fills
   // the chip; 256x160 8-wave + split-K for long-K problems whose 128x160 grid is under ~1.2 waves of CUs.
   // Measured on MI355X with tools/gemm_bench.py --tile.
   const int nt320 = tm256 * (p.N / 320);
   const int nt160_128 = ((p.M + 127) / 128) * ((p.N + 159) / 160);
-  // The keep-masked A operand (routed FFN down projection) takes the 4x2-wave arrangement (wave tile 64x160: half
-  // the A fragments to mask per wave): 61 vs 69 us at M = 65536, N = 320, K = 1280 (tools/gemm_bench.py --tile 5).
   // (180: the 16x16-level fused QKV, M = 4096 x N = 3840 x K = 1280 -- also SDXL's 32x32 level -- 43.8 vs 49.9 us on
   // 128x160; every other U-Net shape is outside 180..240)
   // 32x32-level projections (M = 16384): the LayerNorm-folded QKV / Q and the plain (no residual) N = 640 GEMM on
@@ -1497,17 +1533,14 @@ int dispatch(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
   // (N = 640) in a same-box tools/gpu_tile_sweep.sh run; the residual / conv shapes measured neutral or slower there
   if ((MODE == MODE_GEMM_LN && p.M >= 8192 && p.M <= 16384 && p.N % 320 == 0) ||
       (MODE == MODE_GEMM && !p.R && p.act == ACT_NONE && p.M >= 8192 && p.M <= 16384 && p.N == 640 && p.K == 640))
-    return launch_tile<128, 320, 2, 4, MODE>(p, ws, ws_floats, s);
-  if (p.N % 320 == 0 && nt320 >= 180) {
-    if constexpr (mode_akeep(MODE)) return launch_tile<256, 320, 4, 2, MODE>(p, ws, ws_floats, s);
-    return launch_tile<256, 320, 2, 4, MODE>(p, ws, ws_floats, s);
-  }
+    return {T128x320, 0, 0};
+  if (p.N % 320 == 0 && nt320 >= 180) return {T256x320, 0, 0};
   // 1-1.25 waves of 128x160 tiles (M = 4096 x N = 1280 projections at the 16x16 level): 64x160 tiles double
   // the grid to two workgroups per CU — 15-18 % faster in isolation (tools/gpu_tiles_all.sh). Convs keep their
   // tiles: with the convs included the same-box pipeline A/B measured 0.5 % slower.
-  if ((MODE == MODE_GEMM || MODE >= MODE_KEEP) && p.N % 160 == 0 && nt160_128 >= 200 && nt160_128 < 320 &&
+  if ((MODE == MODE_GEMM || MODE == MODE_GEMM_LN) && p.N % 160 == 0 && nt160_128 >= 200 && nt160_128 < 320 &&
       p.K <= 5120)
-    return launch_tile<64, 160, 2, 2, MODE>(p, ws, ws_floats, s);
+    return {T64x160, 0, 0};
   // convs (tools/gemm_bench.py --tile/--stages sweep, same box): the 16x16-level 3x3 convs (M = 4096, N = 1280,
   // K = 9 x 1280 / 9 x 2560) on the 8-wave 256x320 tile with a 4-way split-K: 120 / 205 us vs 135 / 237 us on
   // 256x160 with a 2-way split (the 32x32 level's 1280 -> 640 conv stays on 128x160: 207 vs 221 us); the
@@ -1517,46 +1550,90 @@ int dispatch(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
     // 8x8-level 3x3 convs (M = 1024, K = 9 x 1280 / 9 x 2560): 8-wave 128x160 tiles (wave tile 32x80), 2-stage ring
     // (two workgroups per CU), 8-way split-K: 44.6 / 68.2 us vs 51.2 / 72.8 on 256x160 4x2 waves (tile_sweep.py)
     // At one prompt per call (M = 128: 8 tiles) the fixed 8-way split left 64 workgroups streaming ~23 K-steps each
-    // behind a 2-stage ring; such grids (<= 16 tiles) take launch_tile's latency-regime split instead (16-24 ways)
+    // behind a 2-stage ring; such grids (<= 16 tiles) take plan_split's latency-regime split instead (16-24 ways)
     if (p.stride == 1 && p.N % 160 == 0 && p.M <= 1024 && p.K >= 9 * 1280)
-      return launch_tile<128, 160, 4, 2, MODE>(p, ws, ws_floats, s, nt160_128 <= 16 ? 0 : 8, 2);
+      return {T128x160_42, nt160_128 <= 16 ? 0 : 8, 2};
     if (p.stride == 1 && p.N % 320 == 0 && nt320 < 240 && p.K >= 9 * 1280 && p.M >= 2048 && p.M <= 4096)
-      return launch_tile<256, 320, 2, 4, MODE>(p, ws, ws_floats, s);
-    if (p.stride == 2 && p.N % 160 == 0 && p.M >= 8192) return launch_tile<64, 160, 2, 2, MODE>(p, ws, ws_floats, s);
+      return {T256x320, 0, 0};
+    if (p.stride == 2 && p.N % 160 == 0 && p.M >= 8192) return {T64x160, 0, 0};
     // the 32x32 -> 16x16 and 16x16 -> 8x8 downsamplers (M = 4096 / 1024): a 4-way split-K, two workgroups per CU
     // (their strided-tap A loads want the extra waves in flight): 46.1-46.7 vs 65.7-66.3 us and 46.4-46.9 vs
     // 78.4-80.1 us with the auto ~one-per-CU split of 2, on every tile shape (same box)
     if (p.stride == 2 && p.N % 160 == 0 && p.M < 8192) {
-      if (p.M > 2048) return launch_tile<128, 160, 2, 2, MODE>(p, ws, ws_floats, s, 4);
-      // (<= 16 tiles, the 16x16 -> 8x8 downsampler at one prompt: launch_tile's latency-regime split)
+      if (p.M > 2048) return {T128x160, 4, 0};
+      // (<= 16 tiles, the 16x16 -> 8x8 downsampler at one prompt: plan_split's latency-regime split)
       const int nt64 = ((p.M + 63) / 64) * (p.N / 160);
-      return launch_tile<64, 160, 2, 2, MODE>(p, ws, ws_floats, s, nt64 <= 16 ? 0 : 4);
+      return {T64x160, nt64 <= 16 ? 0 : 4, 0};
     }
   }
-  // the keep-masked down projection at one prompt (<= 128 tiles of 128x160): 64x160 tiles -- 22.3 vs 29.5 us at the
-  // 64x64 level (profiles/r05_b1_geglu_keep_tiles.txt). Only below K = 2560: there the plain GEMM of the same shape
-  // takes the same 64x160 tile and split, so keep-masked and masked-then-plain stay bit-identical; at K >= 2560 both
-  // take the 256x160 rule below.
-  if constexpr (mode_akeep(MODE))
-    if (p.N % 160 == 0 && p.K < 2560 && nt160_128 <= 128) return launch_tile<64, 160, 2, 2, MODE>(p, ws, ws_floats, s);
+  // (the keep-masked down projection at one prompt, <= 128 tiles of 128x160, runs on 64x160 tiles through the plain
+  // rule below: 22.3 vs 29.5 us at the 64x64 level, profiles/r05_b1_geglu_keep_tiles.txt)
   if (p.N % 160 == 0 && p.K >= 2560 && nt160_128 < 300 && !(MODE == MODE_CONV && p.stride == 2))
-    return launch_tile<256, 160, 4, 2, MODE>(p, ws, ws_floats, s);
-  if (MODE == MODE_CONV_UP) {
-    if (p.N % 160 == 0) return launch_tile<128, 160, 2, 2, MODE>(p, ws, ws_floats, s);
-    return launch_tile<128, 128, 2, 2, MODE>(p, ws, ws_floats, s);
-  }
+    return {T256x160_42, 0, 0};
+  if (MODE == MODE_CONV_UP) return {p.N % 160 == 0 ? T128x160 : T128x128, 0, 0};
   if constexpr (MODE == MODE_CONV)  // conv_out (N = 8 padded channels): a quarter of 128x64's MFMA padding
-    if (p.N <= 32 && g_narrow) return launch_tile<128, 32, 2, 2, MODE>(p, ws, ws_floats, s);
-  if (p.N <= 64) return launch_tile<128, 64, 2, 2, MODE>(p, ws, ws_floats, s);
+    if (p.N <= 32 && g_narrow) return {T128x32, 0, 0};
+  if (p.N <= 64) return {T128x64, 0, 0};
   if (p.N % 160 == 0) {
     // plain GEMMs under ~one wave of 128x160 tiles take 64x160 at any M: the 64x64 level's K = 320 projections at one
     // prompt (M = 8192, N = 320: 128 tiles) 7.8 vs 10.6 us, 8.4 vs 11.8 with the residual (r05_b1_linear_tiles.txt)
-    if (nt160_128 >= 200 || (p.M > 2048 && MODE != MODE_GEMM)) return launch_tile<128, 160, 2, 2, MODE>(p, ws, ws_floats, s);
-    return launch_tile<64, 160, 2, 2, MODE>(p, ws, ws_floats, s);
+    if (nt160_128 >= 200 || (p.M > 2048 && MODE != MODE_GEMM)) return {T128x160, 0, 0};
+    return {T64x160, 0, 0};
   }
   const int nt128 = ((p.M + 127) / 128) * ((p.N + 127) / 128);
-  if (nt128 >= 200 || p.M > 2048) return launch_tile<128, 128, 2, 2, MODE>(p, ws, ws_floats, s);
-  return launch_tile<64, 128, 2, 2, MODE>(p, ws, ws_floats, s);
+  if (nt128 >= 200 || p.M > 2048) return {T128x128, 0, 0};
+  return {T64x128, 0, 0};
+}
+
+// the tile a masked mode runs the plain GEMM's plan on: the same one where it is instantiated for the mode, with the
+// keep-masked A operand on the 4x2-wave arrangement of 256x320 (wave tile 64x160: half the A fragments to mask per
+// wave, 61 vs 69 us at M = 65536, N = 320, K = 1280); the split stays the plain GEMM's, so the bits do too
+template <int MODE>
+int masked_tile(int t, const GemmParams& p) {
+  if (mode_akeep(MODE) && t == T256x320) return T256x320_42;
+  if (t == T128x320 || t == T128x160_42 || t == T64x320 || t == T128x32) return p.N % 160 == 0 ? T128x160 : T128x128;
+  return t;
+}
+
+template <int MODE>
+int launch_plan(int tile, int ksplit, int stages_want, const GemmParams& p, float* ws, hipStream_t s) {
+  switch (tile) {
+    case T128x160: return launch_tile<128, 160, 2, 2, MODE>(p, ws, s, ksplit, stages_want);
+    case T64x160: return launch_tile<64, 160, 2, 2, MODE>(p, ws, s, ksplit, stages_want);
+    case T256x320: return launch_tile<256, 320, 2, 4, MODE>(p, ws, s, ksplit, stages_want);
+    case T256x160_42: return launch_tile<256, 160, 4, 2, MODE>(p, ws, s, ksplit, stages_want);
+    case T256x320_42: return launch_tile<256, 320, 4, 2, MODE>(p, ws, s, ksplit, stages_want);
+    case T128x320: return launch_tile<128, 320, 2, 4, MODE>(p, ws, s, ksplit, stages_want);
+    case T128x64: return launch_tile<128, 64, 2, 2, MODE>(p, ws, s, ksplit, stages_want);
+    case T128x128: return launch_tile<128, 128, 2, 2, MODE>(p, ws, s, ksplit, stages_want);
+    case T64x128: return launch_tile<64, 128, 2, 2, MODE>(p, ws, s, ksplit, stages_want);
+    default: break;
+  }
+  if constexpr (MODE == MODE_GEMM || MODE == MODE_CONV || MODE == MODE_GEMM_LN) {
+    if (tile == T128x160_42) return launch_tile<128, 160, 4, 2, MODE>(p, ws, s, ksplit, stages_want);
+    if (tile == T64x320) return launch_tile<64, 320, 2, 4, MODE>(p, ws, s, ksplit, stages_want);
+  }
+  if constexpr (MODE == MODE_CONV)
+    if (tile == T128x32) return launch_tile<128, 32, 2, 2, MODE>(p, ws, s, ksplit, stages_want);
+  return SDMOE_EUNSUP;
+}
+
+// plan of a dense or masked launch: {tile, split, stages wish}; masked modes plan as the plain GEMM of the shape
+template <int MODE>
+Plan plan_launch(const GemmParams& p, const float* ws, long ws_floats, int* ksplit) {
+  constexpr bool MASKED = mode_akeep(MODE) || mode_wmask(MODE);
+  constexpr int PM = MASKED ? MODE_GEMM : MODE;
+  Plan pl = choose_tile<PM>(p);
+  *ksplit = plan_split(kTile[pl.tile], PM, p, ws, ws_floats, pl.ks_want);
+  if constexpr (MASKED) pl.tile = masked_tile<MODE>(pl.tile, p);
+  return pl;
+}
+
+template <int MODE>
+int dispatch(const GemmParams& p, float* ws, long ws_floats, hipStream_t s) {
+  int ksplit = 1;
+  const Plan pl = plan_launch<MODE>(p, ws, ws_floats, &ksplit);
+  return launch_plan<MODE>(pl.tile, ksplit, pl.stages_want, p, ws, s);
 }
 
 // ---- elementwise helpers for the GEMM operands ------------------------------------------------------
@@ -1786,6 +1863,31 @@ extern "C" int sdmoe_linear_masked(const void* A, long lda, const void* keep, co
   if (keep) return dispatch<MODE_KEEP>(p, workspace, workspace_floats, s);
   if (wmask) return dispatch<MODE_WMASK>(p, workspace, workspace_floats, s);
   return dispatch<MODE_GEMM>(p, workspace, workspace_floats, s);
+}
+
+extern "C" int sdmoe_gemm_plan(int mode, int M, int N, int K, int has_residual, int act, long workspace_floats,
+                               int* out) {
+  if (!out || M <= 0 || N <= 0 || K <= 0 || workspace_floats < 0) return SDMOE_EARG;
+  if (K % 64 || N % 8) return SDMOE_ESHAPE;
+  GemmParams p{};
+  p.M = M; p.N = N; p.K = K; p.act = act; p.rows_per_batch = 1;
+  static const half_t dummy[8] = {};
+  p.R = has_residual ? dummy : nullptr;  // (only its presence enters the plan)
+  // a non-null stand-in for the workspace pointer: only its presence and size enter the plan
+  float* ws = workspace_floats > 0 ? reinterpret_cast<float*>(out) : nullptr;
+  int ksplit = 1;
+  Plan pl;
+  switch (mode) {
+    case MODE_GEMM: pl = plan_launch<MODE_GEMM>(p, ws, workspace_floats, &ksplit); break;
+    case MODE_KEEP: pl = plan_launch<MODE_KEEP>(p, ws, workspace_floats, &ksplit); break;
+    case MODE_WMASK: pl = plan_launch<MODE_WMASK>(p, ws, workspace_floats, &ksplit); break;
+    case MODE_KEEPW: pl = plan_launch<MODE_KEEPW>(p, ws, workspace_floats, &ksplit); break;
+    case MODE_GEMM_LN: pl = plan_launch<MODE_GEMM_LN>(p, nullptr, 0, &ksplit); break;  // (as sdmoe_linear_ln)
+    default: return SDMOE_EUNSUP;
+  }
+  const TileShape& t = kTile[pl.tile];
+  out[0] = t.bm; out[1] = t.bn; out[2] = t.wmw; out[3] = t.wnw; out[4] = ksplit;
+  return SDMOE_OK;
 }
 
 extern "C" int sdmoe_linear_keep(const void* A, long lda, const void* keep, const void* W, long ldw, const void* bias,

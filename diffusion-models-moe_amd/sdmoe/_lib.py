@@ -41,6 +41,7 @@ SIGNATURES = {
     "sdmoe_moe_topk_keep": [_I, _I, _I, _I, _I, _P, _L, _P, _P, _P, _P],
     "sdmoe_linear_keep": [_P, _L, _P, _P, _L, _P, _P, _L, _P, _L, _I, _I, _I, _P, _L, _P],
     "sdmoe_linear_masked": [_P, _L, _P, _P, _L, _P, _P, _P, _L, _P, _L, _I, _I, _I, _P, _L, _P],
+    "sdmoe_gemm_plan": [_I, _I, _I, _I, _I, _I, _L, _P],
     "sdmoe_wmask_kmajor": [_P, _L, _I, _I, _P, _P, _P],
     "sdmoe_timestep_embedding": [_P, _P, _F, _I, _I, _F, _P],
     "sdmoe_cfg_multistep_step": [_P, _L, _P, _I, _I, _I, _F, _P, _P, _P, _P, _P, _L, _P],

@@ -9,6 +9,7 @@ slices of a concatenation buffer, fused QKV outputs); spatial tensors are NHWC f
 """
 from __future__ import annotations
 
+import ctypes
 import os
 
 import torch
@@ -127,6 +128,19 @@ def wmask_kmajor(bits, perm=None, out=None):
                                 _dev(out, "out", torch.int64), _stream())
     _lib.check(st, "sdmoe_wmask_kmajor")
     return out
+
+
+GEMM_PLAN_MODES = {"plain": 0, "keep": 4, "wmask": 5, "keepw": 6, "ln": 7}
+
+
+def gemm_plan(mode, M, N, K, residual=False, act=ACT_NONE, workspace_floats=WS_FLOATS):
+    """The launch sdmoe_linear / _linear_masked / _linear_ln would make for an M x N x K product (sdmoe_gemm_plan,
+    host-only: no device needed): {"tile": (rows, cols), "waves": (along M, along N), "ksplit": k}."""
+    lib = _lib.load()
+    out = (ctypes.c_int * 5)()
+    _lib.check(lib.sdmoe_gemm_plan(GEMM_PLAN_MODES[mode], M, N, K, int(bool(residual)), act, workspace_floats, out),
+               "sdmoe_gemm_plan")
+    return {"tile": (out[0], out[1]), "waves": (out[2], out[3]), "ksplit": out[4]}
 
 
 def linear_masked(x, w, bias=None, *, keep=None, wmask=None, residual=None, out=None):

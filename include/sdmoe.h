@@ -234,6 +234,17 @@ int sdmoe_linear_masked(const void* A, long lda, const void* keep, const void* W
                         float* workspace, long workspace_floats, void* stream);
 
 /*
+ * sdmoe_gemm_plan — host-only query (no device memory, no launch): the launch sdmoe_linear (mode 0),
+ * sdmoe_linear_masked with keep (4), wmask (5) or both (6), or sdmoe_linear_ln (7) would make for an M x N x K
+ * product with / without a residual and activation act, given workspace_floats of split-K workspace (0 = none):
+ * out[0..4] = tile rows, tile columns, waves along M, waves along N, split-K factor. Masked modes take the plain
+ * GEMM's plan (its split, hence each output's fp32 summation order), so sdmoe_linear_masked is bit-identical to
+ * masking A / W first and calling sdmoe_linear; the tests check that over every U-Net shape. Splits depend on the
+ * device's CU count (256 on MI355X, also the value without a device).
+ */
+int sdmoe_gemm_plan(int mode, int M, int N, int K, int has_residual, int act, long workspace_floats, int* out);
+
+/*
  * sdmoe_wmask_kmajor — packed Wanda bits [N][K/8] (row stride ldb bytes; bit k%8 of byte (n, k/8) = W[n, k] removed;
  * the layout of the reference's [C, 4C] masks bit-packed, sdmoe/mask_io.py) -> out [K/64][N] 64-bit words for
  * sdmoe_linear_masked. perm (nullable, int32 [K]) permutes the columns: bit j of word (s, n) = mask(n, perm[64 s + j])

@@ -412,7 +412,7 @@ def test_conv3x3_full_size_tiles(tile, stages):
                                                 (16, 1280, 1280, 16, False), (16, 2560, 1280, 2, False),
                                                 (16, 640, 1280, 3, False), (32, 640, 640, 16, True),
                                                 (32, 640, 640, 2, True), (16, 1280, 1280, 16, True),
-                                                (8, 1280, 1280, 3, True)])
+                                                (16, 1280, 1280, 2, True), (8, 1280, 1280, 3, True)])
 def test_conv3x3_halo_tiles(H, Cin, Cout, nimg, up):
     """Halo-tiled stride-1 convs (MODE_CONVH64/32/16 and the 2x-upsample MODE_CONVHUP64/32/16, every sdmoe_tune knob 16
     setting): the input halo of each 32-channel slice staged once for the 9 taps, incl. image borders, K split over
@@ -509,12 +509,12 @@ def test_groupnorm_full_size(C, HW):
     close(y, F.silu(ref.permute(0, 2, 1).reshape(nimg * HW, C)), tol=5e-3)
 
 
-@pytest.mark.parametrize("tile", [0, 1, 7])
-def test_geglu_fused_full_size(tile):
+@pytest.mark.parametrize("M,C,E,tile", [(65536, 320, 64, 0), (65536, 320, 64, 1), (65536, 320, 64, 7),
+                                        (512, 1280, 256, 0)])
+def test_geglu_fused_full_size(M, C, E, tile):
     """The 64x64 level's fused projection + ReLU GEGLU + expert scores at M = 65,536 (F = 1280, 64 experts of 20)
     against the unfused projection GEMM + route kernel: bit-identical, on the auto tile and the 128x160 4- and
-    8-wave tiles."""
-    M, C, E = 65536, 320, 64
+    8-wave tiles; and the 16x16 level at one prompt (M = 512, F = 5120: the auto rule's 8-wave 128x160 tiles)."""
     F_ = 4 * C
     g = torch.Generator().manual_seed(77)
     x = torch.randn(M, C, generator=g).half().to(DEV)

@@ -50,11 +50,14 @@ def psnr(got, ref, peak=None):
     return float("inf") if mse == 0 else 10 * np.log10(peak * peak / mse)
 
 
-def same_input_recorder(cls):
-    """Receiver subclass recording every hooked call's (t, l, input rows, device selection bits, device scores).
+def same_input_recorder(cls, steps=None):
+    """Receiver subclass recording every hooked call's (t, l, input rows, device selection bits, device scores) -- of
+    the timesteps in `steps` only, when given (the others run cls.hook_fn untouched).
     It routes exactly as cls.hook_fn (same removal lookup, same fused path); only sel_out/score_out are added."""
     class Rec(cls):
         def hook_fn(self, module, input, output):
+            if steps is not None and self.timestep not in steps:
+                return super().hook_fn(module, input, output)
             x = input[0]
             E = module.patterns.shape[0]
             rows = x.numel() // x.shape[-1]

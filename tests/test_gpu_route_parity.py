@@ -274,6 +274,46 @@ def test_keep_mask_in_down_projection_bit_exact(M, C, E, k, nrem, N):
     assert torch.equal(y, y_ref)
 
 
+def _unet_down_shapes():
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from unet_shapes import down_projection_shapes
+    return [("sd14",) + s for s in down_projection_shapes("sd14")] + [("sdxl",) + s for s in down_projection_shapes("sdxl")]
+
+
+@pytest.mark.parametrize("model,M,K,N", _unet_down_shapes())
+def test_masked_down_projection_bit_exact_every_unet_shape(model, M, K, N):
+    """Every FFN down projection SD-1.4 (512^2) and SDXL (1024^2) issue at 1 / 2 / 8 / 16 prompts per call
+    (tests/unet_shapes.py): the keep-masked product (sdmoe_linear_keep) equals top-k-masking the GEGLU product first and
+    running sdmoe_linear, and with a Wanda mask as well (sdmoe_linear_masked, keep + wmask) it equals the plain GEMM
+    on the masked product and the masked weight -- bit for bit, +bias +residual. (Both hold because the masked launch
+    takes the plain GEMM's split-K plan, sdmoe_gemm_plan; test_host_logic checks the plans over a wider sweep.)"""
+    g = torch.Generator().manual_seed(M + K + N)
+    C, F = N, K
+    E = F // 20
+    k = int(E * 0.2)
+    act = ops.ACT_RELU if model == "sd14" else ops.ACT_GELU
+    x = torch.randn(M, C, generator=g).half().to(DEV)
+    w = (torch.randn(2 * F, C, generator=g) * C ** -0.5).half().to(DEV)
+    b = (torch.randn(2 * F, generator=g) * 0.3).half().to(DEV)
+    wd = (torch.randn(N, F, generator=g) * F ** -0.5).half().to(DEV)
+    bd = (torch.randn(N, generator=g) * 0.1).half().to(DEV)
+    res = torch.randn(M, N, generator=g).half().to(DEV)
+    routing = ops.Routing(torch.randperm(F, generator=g) % E, E, k, DEV)
+    removed = ops.removed_bits(torch.randperm(E, generator=g)[:E // 10].tolist(), E, DEV)
+    w_il, b_il = ops.interleave_geglu(w, b, routing.perm)
+    score = torch.empty((M, E), dtype=torch.float16, device=DEV)
+    P = ops.linear_geglu(x, w_il, b_il, act, score=score, esize=routing.esize)
+    keep = ops.moe_topk_keep(score, routing, M, removed=removed)
+    y = ops.linear_keep(P, keep, wd, bd, residual=res)
+    ops.moe_topk_mask(P, score, routing, removed=removed)  # P -> the top-k-masked product, in place
+    assert torch.equal(y, ops.linear(P, wd, bd, residual=res)), "keep-masked vs mask-then-plain"
+    # + a Wanda mask on the down projection's weight (config 4's fused form): ~2.5 % of the weights removed
+    bits = (torch.rand(N, F, generator=g) < 0.025)
+    packed = torch.from_numpy(np.packbits(bits.numpy(), axis=1, bitorder="little")).to(DEV)
+    yw = ops.linear_keep(P, keep, wd, bd, residual=res, wmask=ops.wmask_kmajor(packed))
+    assert torch.equal(yw, ops.linear(P, ops.mask_weight(wd, packed), bd, residual=res)), "keep+wmask vs masked-then-plain"
+
+
 @pytest.mark.parametrize("M,E,k,nrem", [(4096, 256, 51, 20), (1000, 64, 12, 5), (16384, 128, 25, 0), (16385, 128, 25, 3)])
 def test_topk_one_token_per_wave_matches_four(M, E, k, nrem):
     """The top-k kernels at one token per wave (M <= 16384, default) and four per wave (sdmoe_tune knob 15 = 4):

@@ -187,3 +187,95 @@ def test_pipeline_remove_experts_sdxl_base_128x128(act, parity_report):
                   oracle_trunk_clear_disagree=stats["clear_disagree"], rel_l2=rel_l2(got, exp))
     assert stats["clear_disagree"] == 0, stats
     assert rel_l2(got, exp) <= 1e-3
+
+
+CUTOFF_SAMPLE = (0, 19, 20)  # first step, last step with removal (t < 20), first without (remove_skilled_experts.py:32)
+
+
+def test_trajectory_remove_experts_sdxl_base_128x128_bench_shape(parity_report):
+    """BASELINE config 5 at the config-5 bench's own shape (bench.py --model sdxl: 2 prompts per call, U-Net batch 4,
+    SDXL-base 1024^2, GELU FFN, top-k 0.2, expert 20) for 21 DDIM steps, so the RemoveExperts cut-off is crossed: every
+    (t, l) of t = 0..20 carries a non-empty removal list, which the receiver must apply for t < 20 and ignore at t = 20
+    (/root/reference/neuron_receivers/remove_skilled_experts.py:32 `if ... self.timestep < 20`).
+    At t in CUTOFF_SAMPLE (the oracle's fp16 CPU projections make every call cost seconds; 3 of the 21 steps):
+    (1) same-input selection on all 70 hooked calls (check_same_input: identical on every clear row and every row
+        with bit-equal scores, >= 95 % compared, near-tie flips <= 1e-4 of the rows) -- at t = 20 against the
+        reference's UNremoved top-k;
+    (2) the trunk: the fp32 oracle U-Net evaluated on the device's own fp16 U-Net input of that step (prompt 0's
+        uncond + cond images), the device's selection teacher-forced, vs the device's eps: rel L2 <= 2e-3 and
+        max|eps - ref| <= 3e-2 max(1, max|ref|); and the oracle's own top-k on its trunk agrees with the device's on
+        every row clear of a 16-ulp near-tie.
+    The 21-step trajectory as a whole is the device's own (the SD-1.4 50-step test checks the compounding error)."""
+    from neuron_receivers import GEGLU, RemoveExperts
+    from conftest import heartbeat
+    from test_gpu_metric_parity import same_input_recorder, check_same_input, teacher_forced_factory
+    from test_gpu_unet import sel_bits_to_bool
+    act, T, B = "gelu", 21, 2
+    cfg = UNetConfig.sdxl(128)
+    with heartbeat("sdxl-128 x21 weights"):
+        unet, ref = build_rounded(cfg, seed=9)
+    pipe = StableDiffusionPipeline(unet, DEV, num_inference_steps=T)
+    layers = moefy_tiny(pipe, topk=0.2, expert_size=20, relu=False)
+    mods = [m for n, m in pipe.unet.named_modules() if n.endswith("ff.net.0")]
+    L = len(layers)
+    assert L == 70
+    g = torch.Generator().manual_seed(17)
+    lists = {t: {l: sorted(torch.randperm(layers[l][1], generator=g)[:layers[l][1] // 10].tolist()) for l in range(L)}
+             for t in range(T)}
+    assert all(lists[20][l] for l in range(L))  # the t = 20 lists exist and must be ignored
+    rec = same_input_recorder(RemoveExperts, steps=CUTOFF_SAMPLE)(0, None, T, L, replace_fn=GEGLU,
+                                                                    expert_indices=lists, store_gates=False)
+    rec.records = []
+    # the U-Net input / output of the sampled evaluations (fp16 x_in channels 0..3 before, eps channels 0..3 after)
+    evals = []
+    orig = unet.forward_nhwc
+
+    def forward_rec(x_in, t, ctx2d, out=None, **kw):
+        s = len(evals)
+        keep = s in CUTOFF_SAMPLE
+        xin = x_in[:, :4].float().cpu() if keep else None
+        r = orig(x_in, t, ctx2d, out=out, **kw)
+        evals.append((float(t), xin, r[:, :4].float().cpu()) if keep else None)
+        return r
+    unet.forward_nhwc = forward_rec
+    prompts = ["a photograph of an astronaut riding a horse", "a watercolor of a lighthouse at dusk"]
+    try:
+        out, _ = rec.observe_activation(pipe, prompts)
+        torch.cuda.synchronize()
+    finally:
+        del unet.forward_nhwc
+    assert (rec.timestep, rec.layer) == (T, 0) and len(evals) == T
+    assert len(rec.records) == L * len(CUTOFF_SAMPLE)
+    assert all(m._out_keep is not None for m in mods), "fused routed path did not run"
+    assert all(torch.isfinite(o).all() for o in out)
+    with heartbeat("sdxl-128 x21 same-input"):
+        tot = check_same_input(rec.records, mods, lists, act,
+                               report=lambda **t: parity_report("same_input_selection_sdxl_base_128x128_b2_t21", **t))
+    assert tot["calls"] == L * len(CUTOFF_SAMPLE)
+    # device selection of prompt 0's two images (uncond 0, cond B) per sampled (step, layer), for teacher forcing
+    HW = cfg.sample_size ** 2
+    sels = {}
+    for t, l, _, sb, _ in rec.records:
+        E = mods[l].patterns.shape[0]
+        sel = sel_bits_to_bool(sb, E)
+        tok = sel.shape[0] // (2 * B)
+        sels[t * L + l] = sel.reshape(2 * B, tok, E)[[0, B]].reshape(-1, E)
+    rec.records = None
+    ctx, ac = xl_inputs(cfg, prompts[:1])
+    stats = dict(rows=0, clear=0, clear_disagree=0)
+    factory = teacher_forced_factory(layers, act, sels, lists, stats)
+    worst = {}
+    for s in CUTOFF_SAMPLE:
+        t, xin, eps_dev = evals[s]
+        x = xin.reshape(2 * B, cfg.sample_size, cfg.sample_size, 4)[[0, B]].permute(0, 3, 1, 2).contiguous()
+        e_dev = eps_dev.reshape(2 * B, cfg.sample_size, cfg.sample_size, 4)[[0, B]].permute(0, 3, 1, 2)
+        with heartbeat(f"sdxl-128 x21 oracle step {s}"):
+            e_ref = ref(x, t, ctx, added_cond=ac, ff_hook=factory(s))
+        worst[s] = (rel_l2(e_dev, e_ref), max_rel(e_dev, e_ref))
+    parity_report("trunk_sdxl_base_128x128_b2_t21", rows=stats["rows"], clear=stats["clear"],
+                  oracle_trunk_clear_disagree=stats["clear_disagree"],
+                  **{f"eps_rel_l2_t{s}": v[0] for s, v in worst.items()},
+                  **{f"eps_max_rel_t{s}": v[1] for s, v in worst.items()})
+    assert stats["clear_disagree"] == 0, stats
+    for s, (r2, mr) in worst.items():
+        assert r2 <= 2e-3 and mr <= 3e-2, (s, r2, mr)

@@ -569,3 +569,37 @@ def test_geglu_rows_layout():
     w = torch.randn(2 * F, 8)
     w_il, _ = ops.interleave_geglu(w, None, perm)
     assert torch.equal(w_il[0], w[perm[0]]) and torch.equal(w_il[2], w[F + perm[0]]) and torch.equal(w_il[5], w[perm[3]])
+
+
+def test_masked_gemm_plans_take_the_plain_split():
+    """Keep-/Wanda-masked down projections are bit-identical to mask-then-sdmoe_linear only if they split K the same
+    way (the split fixes each output's fp32 summation order; tile and wave shape do not). sdmoe_gemm_plan derives the
+    masked launch from the plain GEMM's plan; this checks it over every FFN down projection SD-1.4 and SDXL issue at
+    1 / 2 / 8 / 16 prompts per call, with and without the residual, plus a sweep of other shapes (M tails, the
+    768px one-image shape M = 9216 of ADVICE r05, K up to 10240)."""
+    from unet_shapes import down_projection_shapes
+    from sdmoe import ops
+    shapes = down_projection_shapes("sd14") + down_projection_shapes("sdxl")
+    assert (8192, 1280, 320) in shapes and (131072, 2560, 640) in shapes  # SD-1.4 B = 1 64x64, SDXL B = 16 64x64
+    sweep = [(m, k, n) for m in (64, 128, 200, 512, 1000, 2048, 4096, 6000, 9216, 16384, 40000, 65536)
+             for k in (320, 1280, 2560, 5120, 10240) for n in (320, 640, 1280)]
+    for M, K, N in shapes + sweep:
+        for res in (False, True):
+            plain = ops.gemm_plan("plain", M, N, K, residual=res)
+            for mode in ("keep", "wmask", "keepw"):
+                got = ops.gemm_plan(mode, M, N, K, residual=res)
+                assert got["ksplit"] == plain["ksplit"], (mode, M, K, N, res, got, plain)
+    # the U-Net's own shapes keep the tiles they were tuned on: 4x2 waves on 256x320 for the keep-masked A operand
+    assert ops.gemm_plan("keep", 65536, 320, 1280) == {"tile": (256, 320), "waves": (4, 2), "ksplit": 1}
+    assert ops.gemm_plan("plain", 65536, 320, 1280)["waves"] == (2, 4)
+    assert ops.gemm_plan("keep", 8192, 320, 1280)["tile"] == (64, 160)    # one prompt, 64x64 level
+    assert ops.gemm_plan("keep", 1024, 1280, 5120)["tile"] == (256, 160)  # 8 prompts, mid block
+    # no empty trailing split (ADVICE r05): every split gets >= 1 K-step
+    for M, K, N in sweep:
+        ks = ops.gemm_plan("plain", M, N, K)["ksplit"]
+        nk = K // 64
+        kchunk = -(-nk // ks)
+        assert (ks - 1) * kchunk < nk, (M, K, N, ks)
+    # without a workspace nothing splits; sdmoe_linear_ln never splits
+    assert ops.gemm_plan("plain", 128, 1280, 5120, workspace_floats=0)["ksplit"] == 1
+    assert ops.gemm_plan("ln", 128, 1280, 1280)["ksplit"] == 1

@@ -5,7 +5,8 @@
 #   none         --mask none (config 2, MOEFy)       b1 / b1none  --batch 1 with / without the mask (configs 3 / 2 at
 #                                                    the reference's one-prompt-per-call shape, base_receiver.py:73)
 #   prof         rocprofv3 --kernel-trace --stats of the metric run (prof_union / prof_sdxl likewise)
-#   pmc          FETCH_SIZE / WRITE_SIZE passes of a 2-step metric run -> pmc_conv_traffic.json
+#   pmc / pmc_b1 FETCH_SIZE / WRITE_SIZE passes of a 2-step metric run (8 / 1 prompts per GPU) ->
+#                pmc_conv_traffic.json / pmc_conv_traffic_b1.json (bench.py picks the one of its --batch)
 # usage: gpurun -- bash tools/gpu_measure.sh TAG STEP...   (default steps: bench union prof)
 set -u
 TAG=${1:-rXX}
@@ -54,14 +55,15 @@ for s in $STEPS; do
       cd $R
       python tools/trace_seq.py $(find $O/$s -name '*kernel_trace.csv' | head -1) --out $O/${s}_seq.txt > /dev/null && head -3 $O/${s}_seq.txt
       rm -rf $O/$s ;;
-    pmc)
+    pmc|pmc_b1)  # FETCH_SIZE / WRITE_SIZE passes of the metric workload (pmc: 8 prompts/GPU; pmc_b1: one prompt)
+      [ $s = pmc_b1 ] && { bb=1; sfx=_b1; } || { bb=8; sfx=; }
       cd /tmp && export TMPDIR=/tmp
       for c in FETCH_SIZE WRITE_SIZE; do
-        timeout -s KILL 300 rocprofv3 --pmc $c -d $O/pmc_$c -o run --output-format csv -- python3 $R/bench.py --inference-steps 2 --steps 1 --warmup 0 --no-cpu-baseline --no-roofline --e2e-steps 0 > $O/pmc_$c.log 2>&1 || { echo "pmc $c failed"; exit 1; }
+        timeout -s KILL 300 rocprofv3 --pmc $c -d $O/${s}_$c -o run --output-format csv -- python3 $R/bench.py --batch $bb --inference-steps 2 --steps 1 --warmup 0 --no-cpu-baseline --no-roofline --e2e-steps 0 > $O/${s}_$c.log 2>&1 || { echo "pmc $c failed"; exit 1; }
       done
       cd $R
-      python tools/pmc_traffic.py $(find $O/pmc_FETCH_SIZE -name '*counter_collection.csv' | head -1) $(find $O/pmc_WRITE_SIZE -name '*counter_collection.csv' | head -1) --out $O/pmc_conv_traffic.json --build "$(cat $R/.build_rev 2>/dev/null)"
-      for c in FETCH_SIZE WRITE_SIZE; do gzip -c $(find $O/pmc_$c -name '*counter_collection.csv' | head -1) > $O/pmc_$c.csv.gz; rm -rf $O/pmc_$c; done ;;
+      python tools/pmc_traffic.py $(find $O/${s}_FETCH_SIZE -name '*counter_collection.csv' | head -1) $(find $O/${s}_WRITE_SIZE -name '*counter_collection.csv' | head -1) --out $O/pmc_conv_traffic$sfx.json --build "$(cat $R/.build_rev 2>/dev/null)" --model sd14 --batch $bb --mask remove
+      for c in FETCH_SIZE WRITE_SIZE; do gzip -c $(find $O/${s}_$c -name '*counter_collection.csv' | head -1) > $O/${s}_$c.csv.gz; rm -rf $O/${s}_$c; done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -39,6 +39,11 @@ def main():
                     "upsample, 9-11 halo conv, 12-14 halo conv with fused upsample); '' = any")
     ap.add_argument("--out", default=None)
     ap.add_argument("--build", default="", help="git revision of the measured build (recorded in the json)")
+    # the bench workload the PMC passes profiled: bench.py attaches roofline.traffic only to a line of the same
+    # model / prompts per GPU / mask (a B = 8 figure on a --batch 1 line would be mislabelled evidence)
+    ap.add_argument("--model", default="sd14")
+    ap.add_argument("--batch", type=int, required=True, help="bench.py --batch of the profiled run (prompts per GPU)")
+    ap.add_argument("--mask", default="remove")
     a = ap.parse_args()
     fetch, names = load(a.fetch_csv, "FETCH_SIZE")
     write, wnames = load(a.write_csv, "WRITE_SIZE")
@@ -78,7 +83,7 @@ def main():
            "fetch_bytes_per_launch": fetch_b, "write_bytes_per_launch": write_b,
            "bytes_per_launch": fetch_b + write_b,
            "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), WRITE_SIZE x1; KiB -> bytes",
-           "build": a.build}
+           "build": a.build, "model": a.model, "batch": a.batch, "mask": a.mask}
     print(json.dumps(res, indent=1))
     if a.out:
         json.dump(res, open(a.out, "w"), indent=1)
