@@ -203,7 +203,7 @@ def test_trajectory_remove_experts_sdxl_base_128x128_bench_shape(parity_report):
         reference's UNremoved top-k;
     (2) the trunk: the fp32 oracle U-Net evaluated on the device's own fp16 U-Net input of that step (prompt 0's
         uncond + cond images), the device's selection teacher-forced, vs the device's eps: rel L2 <= 2e-3 and
-        max|eps - ref| <= 3e-2 max(1, max|ref|); and the oracle's own top-k on its trunk agrees with the device's on
+        max|eps - ref| <= 5e-3 max(1, max|ref|) (measured 8.1e-4 / 9.1e-4); and the oracle's own top-k on its trunk agrees with the device's on
         every row clear of a 16-ulp near-tie.
     The 21-step trajectory as a whole is the device's own (the SD-1.4 50-step test checks the compounding error)."""
     from neuron_receivers import GEGLU, RemoveExperts
@@ -278,4 +278,4 @@ def test_trajectory_remove_experts_sdxl_base_128x128_bench_shape(parity_report):
                   **{f"eps_max_rel_t{s}": v[1] for s, v in worst.items()})
     assert stats["clear_disagree"] == 0, stats
     for s, (r2, mr) in worst.items():
-        assert r2 <= 2e-3 and mr <= 3e-2, (s, r2, mr)
+        assert r2 <= 2e-3 and mr <= 5e-3, (s, r2, mr)  # measured <= 8.1e-4 / 9.1e-4 (r06a)
