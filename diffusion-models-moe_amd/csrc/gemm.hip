@@ -478,14 +478,17 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
   const int fr = lane & 15, fg = lane >> 4;
   if constexpr (HALO) {
     // ---- halo-tiled 3x3 conv main loop. Local K-steps: 9 per main 32-channel slice (tap t; the 9 taps unrolled: kh,
-    // kw and the B ring stage t % 3 compile-time), then the folded shortcut's K-steps (32 channels of A2 at the output
-    // pixel each). Per iteration: counted wait for K-step ks's group (its B tile, + its A2 tile on shortcut steps;
-    // the main slice's halo is always older), one barrier, then group(ks + 2) and -- at t = 0 -- the next slice's halo
-    // into the other buffer (read last by the previous slice), then the MFMAs. A2 ring slots: slot s = k2 % 3 lives
-    // in halo buffer (nsl + (s == 2)) % 2 at offset (s == 1) * A2BYTES: slots 0 / 1 are in the buffer the last main
-    // slice does not read (their loads are issued during its taps 7 / 8), slot 2 in the other one (issued after the
-    // first shortcut step's barrier).
-    static_assert(BK == 32 && NSTAGE == 3 && BM % HW_ == 0 && WM % HW_ == 0 && HW_ % 16 == 0 && FM % 2 == 0 &&
+    // kw compile-time), then the folded shortcut's K-steps (32 channels of A2 at the output pixel each). Per step: a
+    // counted wait for the NEXT step's B tile (older pieces -- this step's A2 tile, the halos -- with it), one barrier,
+    // the MFMAs on the fragments read ahead at the end of the previous step (the DMA issue of the step after its first
+    // MFMA group: A2(ks + 2), B(ks + 3), at t = 0 the next slice's halo into the other buffer), then the next step's B
+    // fragments and first A pair. Round 5 read every step's fragments right behind its barrier: PMC of the 64x64
+    // 320 -> 320 conv with the K-loop loads and the epilogue off (profiles/r06b_pmc_conv.txt) put the MFMA pipe at 61 %
+    // busy with 32 % of the wave cycles in s_waitcnt / s_barrier -- ~800 idle cycles per 1280-cycle K-step.
+    // A2 ring slots: slot s = k2 % 3 lives in halo buffer (nsl + (s == 2)) % 2 at offset (s == 1) * A2BYTES: slots 0 / 1
+    // are in the buffer the last main slice does not read (their loads are issued during its taps 7 / 8), slot 2 in the
+    // other one (issued after the first shortcut step's barrier).
+    static_assert(BK == 32 && NSTAGE == 4 && BM % HW_ == 0 && WM % HW_ == 0 && HW_ % 16 == 0 && FM % 2 == 0 &&
                       (!HUP || ((WM / HW_) % 2 == 0 && HR % 2 == 0)),
                   "halo conv tile");
     constexpr int HB_INS = BN / RPP, H_PW = (H_INS + NW - 1) / NW, BH_PW = (HB_INS + NW - 1) / NW;
@@ -531,25 +534,28 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
       for (int j = 0; j < H_PW; ++j)
         if (j * NW + wave < H_INS) bld16(rsA, hbase + hb * HBYTES + (j * NW + wave) * 1024, hvo[j], (unsigned)(c32 * 64));
     };
-    auto issue_group = [&](int ks) {  // local K-step ks: its B tile (+ A2 tile on a shortcut step) into ring slot ks % 3
-      unsigned kb;
-      const int slot = ks % 3;
-      if (ks < 9 * nsl) {  // W columns ((c32 / 2) * 9 + tap) * 64 + (c32 % 2) * 32
-        const int c32 = c_first + ks / 9, tap = ks % 9;
-        kb = (unsigned)(((c32 >> 1) * 9 + tap) * 128 + (c32 & 1) * 64);
-      } else {  // W columns 9 Cin + 32 k2
-        const int k2 = k2_first + ks - 9 * nsl;
-        kb = (unsigned)(18 * p.Cin + 64 * k2);
-        char* const a2s = hbase + ((nsl + (slot == 2 ? 1 : 0)) & 1) * HBYTES + (slot == 1 ? A2BYTES : 0);
-#pragma unroll
-        for (int j = 0; j < A2_PW; ++j)
-          if (j * NW + wave < A2_INS) bld16(rsA2, a2s + (j * NW + wave) * 1024, a2vo[j], (unsigned)(64 * k2));
-      }
+    // B tiles: a 4-slot ring (slot ks % 4), issued three local K-steps ahead; A2 tiles (folded shortcut): three slots
+    // in the halo buffers (slot ks % 3), issued two steps ahead, ahead of the B tile issued at the same point
+    auto issue_b_kb = [&](int ks, unsigned kb) {
 #pragma unroll
       for (int j = 0; j < BH_PW; ++j)
-        if (j * NW + wave < HB_INS) bld16(rsW, bbase + slot * BSTAGE + (j * NW + wave) * 1024, bvo[j], kb);
+        if (j * NW + wave < HB_INS) bld16(rsW, bbase + (ks & 3) * BSTAGE + (j * NW + wave) * 1024, bvo[j], kb);
     };
-    auto group_cnt = [&](int ks) { return ks < 9 * nsl ? b_cnt : b_cnt + a2_cnt; };
+    // W columns of main slice c32 (global 32-channel slice) at tap: ((c32 / 2) * 9 + tap) * 64 + (c32 % 2) * 32; of
+    // shortcut step k2 (local): 9 Cin + 32 (k2_first + k2)
+    auto kb_main = [&](int c32, int tap) { return (unsigned)(((c32 >> 1) * 9 + tap) * 128 + (c32 & 1) * 64); };
+    auto kb_sc = [&](int k2) { return (unsigned)(18 * p.Cin + 64 * (k2_first + k2)); };
+    auto a2_slot = [&](int ks) -> char* {
+      const int slot = ks % 3;
+      return hbase + ((nsl + (slot == 2 ? 1 : 0)) & 1) * HBYTES + (slot == 1 ? A2BYTES : 0);
+    };
+    auto issue_a2 = [&](int ks) {
+      char* const a2s = a2_slot(ks);
+      const int k2 = k2_first + ks - 9 * nsl;
+#pragma unroll
+      for (int j = 0; j < A2_PW; ++j)
+        if (j * NW + wave < A2_INS) bld16(rsA2, a2s + (j * NW + wave) * 1024, a2vo[j], (unsigned)(64 * k2));
+    };
     auto vm_wait = [&](int n) {  // s_waitcnt vmcnt(n) for the wave-uniform n (immediates only; smaller = safe)
       if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
       else if (n == 11) asm volatile("s_waitcnt vmcnt(11)" ::: "memory");
@@ -575,35 +581,6 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
     }
     const unsigned boff = (unsigned)(fr * RB + ((fg ^ swzk(fr)) << 4));
     const int orow_w = (wr * WM) / HW_;  // the wave's first output row within the tile
-    // MFMAs of one K-step: A fragment i from a_at(i), B fragments from sb. pre() (the K-step's LDS-DMA issue) runs
-    // after the first fragment reads are issued: the DMA issue (~60 cycles per piece) then overlaps the reads' LDS
-    // latency instead of delaying them behind the barrier
-    auto mfma_step = [&](const char* sb, auto&& a_at, auto&& pre) {
-      half8 bcur[FN];
-#pragma unroll
-      for (int j = 0; j < FN; ++j) bcur[j] = *reinterpret_cast<const half8*>(sb + boff + 16 * j * RB);
-      half8 a0 = a_at(0), a1 = a_at(1);
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("" ::: "memory");  // keeps the reads ahead of the DMA issue (IR-level code motion)
-      pre();
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int g = 0; g < FM / 2; ++g) {
-        half8 n0 = a0, n1 = a1;
-        if (g + 1 < FM / 2) {
-          n0 = a_at(2 * g + 2);
-          n1 = a_at(2 * g + 3);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[2 * g][j] = mfma16x16x32(bcur[j], a0, acc[2 * g][j]);
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[2 * g + 1][j] = mfma16x16x32(bcur[j], a1, acc[2 * g + 1][j]);
-        __builtin_amdgcn_sched_barrier(0);
-        a0 = n0;
-        a1 = n1;
-      }
-    };
     // GroupNorm(+SiLU) of the main input (sdmoe_conv3x3_gn): this image's per-channel scale / shift go to LDS first;
     // every staged halo slice is then normalised in place -- slice c + 1 at tap 5 of slice c (its pieces are older
     // than that step's group, so landed; nobody reads its buffer before slice c + 1), the first one before its taps.
@@ -649,44 +626,122 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
         }
       }
     };
+    // Issue points: j = -3, -2, -1 in the prologue, j = s after step s's barrier; point j issues A2(j + 2) (a shortcut
+    // step), then B(j + 3), then -- at tap 0 of a slice with a successor -- that successor's halo. Step s's B fragments
+    // and first A pair are read AHEAD, at the end of step s - 1 (so step s's MFMAs start right behind its barrier instead
+    // of behind a burst of LDS reads): the barrier at the start of step s therefore waits for B(s + 1) (and with it
+    // every older piece: A2(s), the halos), issued at point s - 2. Main-slice steps keep the tap compile-time.
+    auto is_sc = [&](int ks) { return ks >= 9 * nsl && ks < nkl; };
+    auto issue_b_any = [&](int ks) {  // (prologue / shortcut steps: runtime tap)
+      if (ks < 9 * nsl) issue_b_kb(ks, kb_main(c_first + ks / 9, ks % 9));
+      else issue_b_kb(ks, kb_sc(ks - 9 * nsl));
+    };
+    half8 bcur[FN], a0, a1;
+    auto read_b = [&](int ks) {  // B fragments of step ks (slot ks % 4)
+      const char* sb = bbase + (ks & 3) * BSTAGE + wc * WN * RB;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bcur[j] = *reinterpret_cast<const half8*>(sb + boff + 16 * j * RB);
+    };
+    auto a_frag = [&](const char* hbuf, auto tc, int i) -> half8 {  // A fragment i at compile-time tap, halo buffer hbuf
+      constexpr int t = decltype(tc)::value, kh = t / 3, kw = t % 3;
+      const int i16 = 16 * i;
+      if constexpr (HUP)  // input row ((orow + kh - 1) >> 1) - (oh0 / 2 - 1), column (ocol0 / 2) + lane part
+        return *reinterpret_cast<const half8*>(hbuf + aoff[kw] + (((((i16 / HW_) + kh - 1) >> 1) + 1) * HP + (i16 % HW_) / 2) * RB);
+      else
+        return *reinterpret_cast<const half8*>(hbuf + aoff[kw] + ((i16 / HW_ + kh) * HP + (i16 % HW_) + kw) * RB);
+    };
+    const int hrow = (HUP ? orow_w / 2 : orow_w) * HP * RB;  // the wave's first halo row
+    // the step's MFMAs on bcur / a0 a1 (already in registers); the rest of the A pairs read one group ahead; mid()
+    // (the step's DMA issue) after the first group, so both waves of a SIMD have matrix work queued while it issues
+    auto mfma_groups = [&](auto&& a_at, auto&& mid) {
+#pragma unroll
+      for (int g = 0; g < FM / 2; ++g) {
+        half8 n0 = a0, n1 = a1;
+        if (g + 1 < FM / 2) {
+          n0 = a_at(2 * g + 2);
+          n1 = a_at(2 * g + 3);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[2 * g][j] = mfma16x16x32(bcur[j], a0, acc[2 * g][j]);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[2 * g + 1][j] = mfma16x16x32(bcur[j], a1, acc[2 * g + 1][j]);
+        __builtin_amdgcn_sched_barrier(0);
+        if (g == 0) {
+          asm volatile("" ::: "memory");
+          mid();
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        a0 = n0;
+        a1 = n1;
+      }
+    };
     if (nkl > 0) {
       if (nsl > 0) issue_halo(c_first, 0);
-      issue_group(0);
-      if (nkl > 1) issue_group(1);
+      if (!(p.diag & 1)) {  // points -3, -2, -1: B(0); A2(0), B(1); A2(1), B(2)
+        issue_b_any(0);
+        if (is_sc(0)) issue_a2(0);
+        if (nkl > 1) issue_b_any(1);
+        if (is_sc(1)) issue_a2(1);
+        if (nkl > 2) issue_b_any(2);
+      }
+      // younger than B(0): A2(0), B(1), A2(1), B(2)
+      const int w0 = (is_sc(0) ? a2_cnt : 0) + (nkl > 1 ? b_cnt : 0) + (is_sc(1) ? a2_cnt : 0) + (nkl > 2 ? b_cnt : 0);
       if (gn && nsl > 0) {  // the first slice's halo (the oldest load) landed, visible to all, normalised
-        vm_wait(nkl > 1 ? group_cnt(0) + group_cnt(1) : group_cnt(0));
+        vm_wait(w0 + b_cnt);
         __syncthreads();
         transform(c_first, 0);
       }
+      vm_wait(w0);
+      __syncthreads();
+      read_b(0);
+      if (nsl > 0) {
+        a0 = a_frag(hbase + hrow, std::integral_constant<int, 0>(), 0);
+        a1 = a_frag(hbase + hrow, std::integral_constant<int, 0>(), 1);
+      }
     }
     for (int cs = 0; cs < nsl; ++cs) {
-      const int hb = cs & 1;
       const bool more = cs + 1 < nsl;
-      const char* hbuf = hbase + hb * HBYTES + (HUP ? orow_w / 2 : orow_w) * HP * RB;
+      const char* const hcur = hbase + (cs & 1) * HBYTES + hrow;
+      const char* const hnxt = hbase + ((cs & 1) ^ 1) * HBYTES + hrow;
+      const int c32 = c_first + cs;
       auto tap_step = [&](auto tc) {
-        constexpr int t = decltype(tc)::value, kh = t / 3, kw = t % 3;
+        constexpr int t = decltype(tc)::value;
         const int ks = cs * 9 + t;
-        // younger than group(ks) (issued at iteration ks - 2): the halo issued at iteration ks - 2 (t == 2) or
-        // ks - 1 (t == 1), and group(ks + 1)
-        int nwait = ks + 1 < nkl ? group_cnt(ks + 1) : 0;
+        // younger than B(ks + 1): the halo issued at point ks - 2 (t == 2) and ks - 1 (t == 1), A2(ks + 1) (the
+        // first shortcut step, t == 8 of the last slice), B(ks + 2)
+        int nwait = ks + 2 < nkl ? b_cnt : 0;
         if ((t == 1 || t == 2) && more) nwait += h_cnt;
-        vm_wait(nwait);
+        if (t == 8 && !more && n2 > 0) nwait += a2_cnt;
+        vm_wait(ks + 1 < nkl ? nwait : 0);
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        auto pre = [&]() {
-          if (ks + 2 < nkl && !(p.diag & 1)) issue_group(ks + 2);
-          if (t == 0 && more && !(p.diag & 1)) issue_halo(c_first + cs + 1, hb ^ 1);
+        if (t == 5 && more && gn) transform(c32 + 1, (cs & 1) ^ 1);
+        auto mid = [&]() {
+          if (p.diag & 1) return;
+          if (t >= 7 && !more && n2 > t - 7) issue_a2(ks + 2);  // A2 of shortcut step t - 7
+          if constexpr (t + 3 < 9) {
+            issue_b_kb(ks + 3, kb_main(c32, t + 3));
+          } else {
+            if (more) issue_b_kb(ks + 3, kb_main(c32 + 1, t - 6));
+            else if (n2 > t - 6) issue_b_kb(ks + 3, kb_sc(t - 6));
+          }
+          if (t == 0 && more) issue_halo(c32 + 1, (cs & 1) ^ 1);
         };
-        if (t == 5 && more && gn) transform(c_first + cs + 1, hb ^ 1);
-        if (p.diag & 2) { pre(); return; }
-        mfma_step(bbase + (t % 3) * BSTAGE + wc * WN * RB, [&](int i) -> half8 {
-          const int i16 = 16 * i;
-          if constexpr (HUP)  // input row ((orow + kh - 1) >> 1) - (oh0 / 2 - 1), column (ocol0 / 2) + lane part
-            return *reinterpret_cast<const half8*>(hbuf + aoff[kw] +
-                                                   (((((i16 / HW_) + kh - 1) >> 1) + 1) * HP + (i16 % HW_) / 2) * RB);
-          else
-            return *reinterpret_cast<const half8*>(hbuf + aoff[kw] + ((i16 / HW_ + kh) * HP + (i16 % HW_) + kw) * RB);
-        }, pre);
+        if (!(p.diag & 2)) mfma_groups([&](int i) -> half8 { return a_frag(hcur, tc, i); }, mid);
+        else mid();
+        // read-ahead of step ks + 1: tap t + 1, or tap 0 of the next slice, or (B only) the first shortcut step
+        if constexpr (t < 8) {
+          read_b(ks + 1);
+          a0 = a_frag(hcur, std::integral_constant<int, t + 1>(), 0);
+          a1 = a_frag(hcur, std::integral_constant<int, t + 1>(), 1);
+        } else {
+          if (ks + 1 < nkl) read_b(ks + 1);
+          if (more) {
+            a0 = a_frag(hnxt, std::integral_constant<int, 0>(), 0);
+            a1 = a_frag(hnxt, std::integral_constant<int, 0>(), 1);
+          }
+        }
       };
       tap_step(std::integral_constant<int, 0>());
       tap_step(std::integral_constant<int, 1>());
@@ -698,19 +753,27 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
       tap_step(std::integral_constant<int, 7>());
       tap_step(std::integral_constant<int, 8>());
     }
-    for (int k2l = 0; k2l < n2; ++k2l) {  // folded shortcut K-steps
-      const int ks = 9 * nsl + k2l, slot = ks % 3;
-      vm_wait(ks + 1 < nkl ? group_cnt(ks + 1) : 0);
+    for (int k2l = 0; k2l < n2; ++k2l) {  // folded shortcut K-steps: B read ahead, the A2 pair right behind the barrier
+      const int ks = 9 * nsl + k2l;
+      // younger than B(ks + 1): A2(ks + 1), B(ks + 2)
+      vm_wait(ks + 1 < nkl ? (is_sc(ks + 1) ? a2_cnt : 0) + (ks + 2 < nkl ? b_cnt : 0) : 0);
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      auto pre = [&]() {
-        if (ks + 2 < nkl && !(p.diag & 1)) issue_group(ks + 2);
+      auto mid = [&]() {
+        if (p.diag & 1) return;
+        if (is_sc(ks + 2)) issue_a2(ks + 2);
+        if (ks + 3 < nkl) issue_b_kb(ks + 3, kb_sc(k2l + 3));
       };
-      if (p.diag & 2) { pre(); continue; }
-      const char* a2s = hbase + ((nsl + (slot == 2 ? 1 : 0)) & 1) * HBYTES + (slot == 1 ? A2BYTES : 0) + wr * WM * RB;
-      mfma_step(bbase + slot * BSTAGE + wc * WN * RB, [&](int i) -> half8 {
-        return *reinterpret_cast<const half8*>(a2s + boff + 16 * i * RB);
-      }, pre);
+      const char* a2s = a2_slot(ks) + wr * WM * RB;
+      auto a2_at = [&](int i) -> half8 { return *reinterpret_cast<const half8*>(a2s + boff + 16 * i * RB); };
+      if (!(p.diag & 2)) {
+        a0 = a2_at(0);
+        a1 = a2_at(1);
+        mfma_groups(a2_at, mid);
+      } else {
+        mid();
+      }
+      if (ks + 1 < nkl) read_b(ks + 1);
     }
   } else {
   // prologue: stages 0 .. NSTAGE-2
@@ -1414,7 +1477,7 @@ int launch_halo(GemmParams p, float* ws, long ws_floats, hipStream_t s) {
   p.epi_direct = g_epi_direct == 2 || (g_epi_direct == 1 && p.R == nullptr);  // host-side: a device test of R spilled
   p.res16 = g_res16;
   (void)HW_;
-  gemm_kernel<BM, 320, 2, 4, MODE, 3, 32><<<dim3(ntiles * p.ksplit), 512, 0, s>>>(p);
+  gemm_kernel<BM, 320, 2, 4, MODE, 4, 32><<<dim3(ntiles * p.ksplit), 512, 0, s>>>(p);
   SDMOE_CHECK_LAUNCH();
   if (p.ksplit > 1) {
     long nchunk = (long)p.M * (p.N / 8);
