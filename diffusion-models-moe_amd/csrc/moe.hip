@@ -407,6 +407,86 @@ __global__ __launch_bounds__(256) void moe_topk_keep_quad_kernel(
   }
 }
 
+// The FULL quad kernel's scheme for E = 16 L experts of 20 neurons with a GROUP of L = 8 / 16 lanes per token (E = 128:
+// the 32x32-level FFNs of SD-1.x and SDXL's 64x64 level; E = 256: the 16x16 / 8x8 levels; 8 / 4 tokens per wave):
+// lane r of a group holds experts 16 r .. 16 r + 15 (= neurons 320 r .. 320 r + 319 = keep words 5 r .. 5 r + 4, a
+// compile-time bit pattern), the 16-bit radix counts are summed over the group with DPP (quad xor 1 / 2, then
+// row_half_mirror, row_mirror: no ballots, no SALU chain, no LDS), ties at the k-th key go to the lowest expert id via
+// a group prefix of the tie counts. Same selection rule and outputs as moe_topk_mask_kernel's keep form, which it
+// replaces for these E (that kernel's one token per wave walked a serial ballot / popcount chain: 13.0 us at M =
+// 16384, E = 128 and 8.5 us at M = 4096, E = 256 in the metric's profile, latency-bound on a few MB).
+template <int L>
+__global__ __launch_bounds__(256) void moe_topk_keep_group_kernel(
+    int M, int F, int E, int k, const half_t* __restrict__ score, long lds, const uint32_t* __restrict__ removed,
+    uint32_t* __restrict__ sel_out, unsigned long long* __restrict__ keep) {
+  static_assert(L == 8 || L == 16, "8 or 16 lanes per token");
+  const int lane = threadIdx.x & 63, r = lane & (L - 1);
+  const int m = blockIdx.x * (256 / L) + (int)(threadIdx.x / L);
+  const int mc = min(m, M - 1);
+  const half_t* srow = score + (long)mc * lds + 16 * r;
+  const half8 a = *reinterpret_cast<const half8*>(srow), b = *reinterpret_cast<const half8*>(srow + 8);
+  const uint32_t rm16 = removed ? (removed[(16 * r) >> 5] >> ((16 * r) & 31)) & 0xffffu : 0u;
+  uint32_t key[16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    key[i] = order_key(((rm16 >> i) & 1u) ? (half_t)0.f : a[i]);
+    key[8 + i] = order_key(((rm16 >> (8 + i)) & 1u) ? (half_t)0.f : b[i]);
+  }
+  auto group_sum = [](uint32_t c) {
+    c += quad_mov<QP_XOR1>(c);
+    c += quad_mov<QP_XOR2>(c);
+    c += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x141, 0xf, 0xf, false);  // row_half_mirror
+    if constexpr (L == 16) c += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x140, 0xf, 0xf, false);  // row_mirror
+    return c;
+  };
+  uint32_t T = 0;
+  for (int bit = 15; bit >= 0; --bit) {
+    const uint32_t cand = T | (1u << bit);
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) c += key[i] >= cand ? 1u : 0u;
+    if ((int)group_sum(c) >= k) T = cand;
+  }
+  uint32_t gt = 0, ties = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    gt += key[i] > T ? 1u : 0u;
+    ties += key[i] == T ? 1u : 0u;
+  }
+  const int need = k - (int)group_sum(gt);
+  // exclusive prefix of the group's tie counts (lower lanes = lower expert ids first): Hillis-Steele inside the group
+  uint32_t inc = ties;
+#pragma unroll
+  for (int d = 1; d < L; d <<= 1) {
+    const uint32_t v = (uint32_t)__shfl_up((int)inc, d, 64);
+    if (r >= d) inc += v;
+  }
+  int rk = (int)(inc - ties);
+  uint32_t sel16 = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const bool tie = key[i] == T;
+    const bool sel = k > 0 && (key[i] > T || (tie && rk < need));
+    rk += tie ? 1 : 0;
+    sel16 |= (sel ? 1u : 0u) << i;
+  }
+  const uint32_t keep16 = sel16 & ~rm16;
+  const uint32_t sel_hi = quad_mov<QP_XOR1>(sel16);  // the odd neighbour's experts (32-expert selection words)
+  if (m >= M) return;
+  if (sel_out && (r & 1) == 0) sel_out[(long)m * (E >> 5) + (r >> 1)] = sel16 | (sel_hi << 16);
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    unsigned long long w = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int lo = max(20 * i, 64 * j) - 64 * j, hi = min(20 * i + 20, 64 * j + 64) - 64 * j;
+      if (hi > lo) w |= ((keep16 >> i) & 1u) ? ((1ull << (hi - lo)) - 1ull) << lo : 0ull;
+    }
+    keep[(long)(5 * r + j) * M + m] = w;
+  }
+  (void)F;
+}
+
 }  // namespace
 
 int g_topk_tpw = 0;  // sdmoe_tune knob 15: 0 = by M (default; keep bits at E <= 64: one quad per token), 1 / 4 =
@@ -470,6 +550,18 @@ extern "C" int sdmoe_moe_topk_keep(int M, int F, int E, int esize, int k, const 
       moe_topk_keep_quad_kernel<false, 20><<<g, 256, 0, s>>>(M, F, E, esize, k, sc, ld_score, rm, sel_out, kp);
     else
       moe_topk_keep_quad_kernel<false, 0><<<g, 256, 0, s>>>(M, F, E, esize, k, sc, ld_score, rm, sel_out, kp);
+    SDMOE_CHECK_LAUNCH();
+    return SDMOE_OK;
+  }
+  if ((E == 128 || E == 256) && esize == 20 && g_topk_tpw == 0 && ld_score % 8 == 0 && ((uintptr_t)score & 15) == 0) {
+    hipStream_t s = (hipStream_t)stream;
+    const half_t* sc = (const half_t*)score;
+    const uint32_t* rm = (const uint32_t*)removed_bits;
+    unsigned long long* kp = (unsigned long long*)keep;
+    if (E == 128)
+      moe_topk_keep_group_kernel<8><<<(M + 31) / 32, 256, 0, s>>>(M, F, E, k, sc, ld_score, rm, sel_out, kp);
+    else
+      moe_topk_keep_group_kernel<16><<<(M + 15) / 16, 256, 0, s>>>(M, F, E, k, sc, ld_score, rm, sel_out, kp);
     SDMOE_CHECK_LAUNCH();
     return SDMOE_OK;
   }

@@ -347,12 +347,18 @@ def test_topk_one_token_per_wave_matches_four(M, E, k, nrem):
 @pytest.mark.parametrize("M,E,k,nrem,esize,ld", [(65536, 64, 12, 5, 20, 64), (4097, 64, 13, 0, 20, 64),
                                                   (1000, 64, 64, 3, 20, 72), (333, 48, 9, 2, 20, 48),
                                                   (70, 32, 6, 1, 20, 33), (129, 64, 0, 0, 20, 64),
-                                                  (500, 64, 12, 4, 10, 64), (256, 16, 4, 0, 40, 16)])
+                                                  (500, 64, 12, 4, 10, 64), (256, 16, 4, 0, 40, 16),
+                                                  (16384, 128, 25, 12, 20, 128), (2049, 128, 25, 0, 20, 136),
+                                                  (77, 128, 128, 5, 20, 128), (4096, 256, 51, 25, 20, 256),
+                                                  (513, 256, 51, 3, 20, 264), (100, 256, 0, 0, 20, 256),
+                                                  (300, 128, 25, 2, 20, 130)])
 def test_topk_keep_quad_kernel(M, E, k, nrem, esize, ld):
-    """sdmoe_moe_topk_keep at E <= 64 (one quad of lanes per token, the default there) vs the ballot kernel (sdmoe_tune
-    knob 15 = 4) and vs a numpy restatement of the selection rule (moefy.py:20-23 top-k; ties at the k-th score
-    toward the lowest expert id; removed experts score 0 and are never kept): identical keep words and selection bits,
-    on scores quantised to force ties, with M tails, strided / unaligned score rows (ld != E), k = 0 and k = E."""
+    """sdmoe_moe_topk_keep at E <= 64 (one quad of lanes per token, the default there) and at E = 128 / 256 with the
+    reference's 20-neuron experts (a group of 8 / 16 lanes per token) vs the ballot kernel (sdmoe_tune knob 15 = 4)
+    and vs a numpy restatement of the selection rule (moefy.py:20-23 top-k; ties at the k-th score toward the lowest
+    expert id; removed experts score 0 and are never kept): identical keep words and selection bits, on scores
+    quantised to force ties, with M tails, strided / unaligned score rows (ld != E; ld % 8 != 0 takes the ballot
+    kernel), k = 0 and k = E."""
     from sdmoe import _lib
     lib = _lib.load()
     g = torch.Generator().manual_seed(M + 7 * E + k)
