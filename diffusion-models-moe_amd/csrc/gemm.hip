@@ -181,7 +181,12 @@ template <int BN, int MODE>
 constexpr int keep_w_bytes() { return mode_wmask(MODE) ? ((BN * 8 + 1023) / 1024) * 1024 : 0; }
 template <int BM, int BN, int MODE>
 constexpr int keep_stage_bytes() { return keep_a_bytes<BM, MODE>() + keep_w_bytes<BN, MODE>(); }
-constexpr int KEEP_LUT_BYTES = 16 * 8;  // 4 keep bits -> 4 x 16-bit lane masks
+// MODE_KEEP: a keep byte (8 neurons) -> 4 x 32-bit masks of the 8 fp16 halves, one ds_read_b128 per A fragment
+// (round 5: two dependent ds_read_b64 from a 16-entry nibble table: keep-masked down projections 1.5-3 % slower);
+// the W-masked modes keep the nibble table (the byte table there cost the 128x160 KEEPW tile its second workgroup
+// per CU: 173 -> 268 VGPRs)
+template <int MODE>
+constexpr int keep_lut_bytes() { return MODE == MODE_KEEP ? 256 * 16 : 16 * 8; }
 
 // Routed-GEGLU expert scores over one staged pass of a wave's tile: the activated gates (fp16) of RG rows x NH
 // neurons, experts = contiguous S-neuron slices (neurons pre-permuted expert-major). score = fp32 sum in neuron order,
@@ -276,8 +281,8 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
   constexpr int EPI = NW * (WM / NPASS) * WN_PAD * 4;
   constexpr int EPI16 = NW * (WM / NPASS16) * RS16 * 2;
   constexpr int SMEM0 = (RINGX > EPI) ? (RINGX > EPI16 ? RINGX : EPI16) : (EPI > EPI16 ? EPI : EPI16);
-  constexpr int LUT_OFF = SMEM0;                 // MODE_KEEP: 16-entry nibble -> lane-mask table behind everything
-  constexpr int SMEM1 = SMEM0 + (KEEP ? KEEP_LUT_BYTES : 0);
+  constexpr int LUT_OFF = SMEM0;                 // MODE_KEEP: 256-entry byte -> lane-mask table behind everything
+  constexpr int SMEM1 = SMEM0 + (KEEP ? keep_lut_bytes<MODE>() : 0);
   // LN: per tile row (rstd, -mean*rstd), then the tile's BN columns of wsum and ln_bias (fp32), behind everything
   constexpr int LN_ROW_OFF = SMEM1, LN_COL_OFF = SMEM1 + BM * 8;
   constexpr int SMEM = SMEM1 + (LN ? BM * 8 + BN * 8 : 0);
@@ -381,8 +386,17 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
     kvoff = kpa ? (unsigned)((m0 + 128 * kpiece) * 8 + lane * 16)
                 : (unsigned)((n0 + 128 * (kpiece - KA_INS)) * 8 + lane * 16);
     kdst = kpa ? KEEP_OFF + kpiece * 1024 : WKEEP_OFF + (kpiece - KA_INS) * 1024;
-    // nibble -> two 16-bit-lane masks: entry e masks halves 0..3 by bits 0..3 of e
-    if (tid < 16) {
+    // byte -> four 32-bit masks: entry e masks fp16 halves 0..7 by bits 0..7 of e (one ds_read_b128 per fragment;
+    // round 5's 16-entry nibble table took two dependent ds_read_b64)
+    if constexpr (MODE == MODE_KEEP) {
+      for (int e = tid; e < 256; e += NT) {
+        uint4v m;
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+          m[d] = (((e >> (2 * d)) & 1) ? 0xFFFFu : 0u) | (((e >> (2 * d + 1)) & 1) ? 0xFFFF0000u : 0u);
+        *reinterpret_cast<uint4v*>(smem + LUT_OFF + e * 16) = m;
+      }
+    } else if (tid < 16) {  // nibble -> two 32-bit masks
       const unsigned lo = ((tid & 1) ? 0xFFFFu : 0u) | ((tid & 2) ? 0xFFFF0000u : 0u);
       const unsigned hi = ((tid & 4) ? 0xFFFFu : 0u) | ((tid & 8) ? 0xFFFF0000u : 0u);
       *reinterpret_cast<uint2v*>(smem + LUT_OFF + tid * 8) = (uint2v){lo, hi};
@@ -818,10 +832,15 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
       half8 a = *reinterpret_cast<const half8*>(sa + row * RB + (((kk * 4 + fg) ^ swzk(row)) << 4));
       if constexpr (AKEEP) {  // zero the neurons of this row's dropped experts (8 neurons = chunk kk*4+fg)
         const unsigned kbyte = *reinterpret_cast<const unsigned char*>(sa + KEEP_OFF + row * 8 + kk * 4 + fg);
-        const uint2v lo = *reinterpret_cast<const uint2v*>(smem + LUT_OFF + (kbyte & 15u) * 8);
-        const uint2v hi = *reinterpret_cast<const uint2v*>(smem + LUT_OFF + (kbyte >> 4) * 8);
         uint4v u = __builtin_bit_cast(uint4v, a);
-        u[0] &= lo[0]; u[1] &= lo[1]; u[2] &= hi[0]; u[3] &= hi[1];
+        if constexpr (MODE == MODE_KEEP) {  // byte table: one ds_read_b128 behind the keep byte
+          const uint4v mk = *reinterpret_cast<const uint4v*>(smem + LUT_OFF + kbyte * 16);
+          u[0] &= mk[0]; u[1] &= mk[1]; u[2] &= mk[2]; u[3] &= mk[3];
+        } else {  // KEEPW: the nibble table (its wider reads cost the 128x160 tile its second workgroup per CU)
+          const uint2v lo = *reinterpret_cast<const uint2v*>(smem + LUT_OFF + (kbyte & 15u) * 8);
+          const uint2v hi = *reinterpret_cast<const uint2v*>(smem + LUT_OFF + (kbyte >> 4) * 8);
+          u[0] &= lo[0]; u[1] &= lo[1]; u[2] &= hi[0]; u[3] &= hi[1];
+        }
         a = __builtin_bit_cast(half8, u);
       }
       return a;
@@ -1407,7 +1426,7 @@ int launch_tile(GemmParams p, float* ws, hipStream_t s, int ksplit, int stages_w
     const int stages = g_stages ? g_stages
                                 : (stages_want ? stages_want : ((WMW * WNW == 4 && ntiles * p.ksplit >= 300) ? 2 : 3));
     constexpr bool FITS3 = 3 * ((BM + BN) * 64 * 2 + 1024 + keep_stage_bytes<BM, BN, MODE>()) +
-                               (keep_stage_bytes<BM, BN, MODE>() ? KEEP_LUT_BYTES : 0) +
+                               (keep_stage_bytes<BM, BN, MODE>() ? keep_lut_bytes<MODE>() : 0) +
                                ((MODE == MODE_GEMM_LN || MODE == MODE_GEGLU_LN) ? BM * 8 + BN * 8 : 0) <= 160 * 1024;
     if constexpr (FITS3) {
       if (stages == 2) gemm_kernel<BM, BN, WMW, WNW, MODE, 2, 64><<<grid, NTH, 0, s>>>(p);
