@@ -827,10 +827,31 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
     const char* sbm = sa + BM * BK * 2;
     if (p.diag & 2) continue;
     // fragment reads (A masked by MoE keep bits, B by Wanda bits where the mode says so)
+    // MODE_KEEP on the software-pipelined tiles: every A fragment's lane mask of the K-step looked up up front, right
+    // behind the barrier (one ds_read_b64 of a fragment row's 8 keep bytes, then one ds_read_b128 per fragment), so the
+    // fragment reads of the loop carry no dependent keep-byte -> table chain (it was exposed behind the 10-MFMA groups
+    // of the 64x160 / 128x160 tiles: keep-masked 16x16-level down projection 49.9 vs 32.5 us plain, loads and epilogue
+    // off)
+    constexpr bool KPRE = MODE == MODE_KEEP && !(KEEP && FN > 5) && BK == 64 && FM <= 4;  // (FM = 8: +64 VGPRs, spills)
+    uint4v kmask[KPRE ? 2 : 1][KPRE ? FM : 1];
+    if constexpr (KPRE) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const uint2v kq = *reinterpret_cast<const uint2v*>(sa + KEEP_OFF + (wr * WM + i * 16 + fr) * 8);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+          kmask[kk][i] = *reinterpret_cast<const uint4v*>(smem + LUT_OFF + ((kq[kk] >> (8 * fg)) & 255u) * 16);
+      }
+    }
     auto read_a = [&](int kk, int i) -> half8 {
       const int row = wr * WM + i * 16 + fr;
       half8 a = *reinterpret_cast<const half8*>(sa + row * RB + (((kk * 4 + fg) ^ swzk(row)) << 4));
-      if constexpr (AKEEP) {  // zero the neurons of this row's dropped experts (8 neurons = chunk kk*4+fg)
+      if constexpr (KPRE) {
+        uint4v u = __builtin_bit_cast(uint4v, a);
+        const uint4v mk = kmask[kk][i];
+        u[0] &= mk[0]; u[1] &= mk[1]; u[2] &= mk[2]; u[3] &= mk[3];
+        a = __builtin_bit_cast(half8, u);
+      } else if constexpr (AKEEP) {  // zero the neurons of this row's dropped experts (8 neurons = chunk kk*4+fg)
         const unsigned kbyte = *reinterpret_cast<const unsigned char*>(sa + KEEP_OFF + row * 8 + kk * 4 + fg);
         uint4v u = __builtin_bit_cast(uint4v, a);
         if constexpr (MODE == MODE_KEEP) {  // byte table: one ds_read_b128 behind the keep byte
