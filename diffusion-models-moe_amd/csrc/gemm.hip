@@ -37,6 +37,9 @@ int g_mfast = 1;   // knob 14: split-K conv grids ordered M-tile fastest (1) or 
 int g_epi_direct = 1;
 int g_cus = 256;  // compute units of the device (device_cus(): hipDeviceAttributeMultiprocessorCount, queried once)
 bool g_cus_init = false;
+#ifndef SDMOE_GEMM_DIAG
+#define SDMOE_GEMM_DIAG 0  // 1: the halo conv loop honours the diagnostics knob too (make DIAG=1)
+#endif
 int g_diag = 0;  // knob 6, diagnostics only (results garbage): bit 0 = no K-loop operand loads, bit 1 = no MFMAs,
                  // bit 4 = no A-operand pieces, bit 5 = no B-operand pieces,
                  // bit 2 = no epilogue (nothing stored), bit 3 = epilogue without its global stores
@@ -512,7 +515,10 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
     const int a2_cnt = p.A2 ? A2_INS / NW + (wave < A2_INS % NW ? 1 : 0) : 0;
     const int pix = (HUP ? 2 * p.H : p.H) * HW_;  // output pixels per image
     const int bimg = m0 / pix, oh0 = (m0 - bimg * pix) / HW_;
-    unsigned hvo[H_PW], bvo[BH_PW], a2vo[A2_PW];
+    // B / A2 pieces j > 0 sit whole 128-row rounds below piece 0 (same swizzle): their offsets go to the scalar
+    // offset (j x bstep / a2step), one VGPR per operand instead of one per piece -- the 256x320 tile has none spare
+    unsigned hvo[H_PW], bvo0, a2vo0;
+    const unsigned bstep = (unsigned)(NW * RPP * p.ldw * 2), a2step = (unsigned)(NW * RPP * p.lda2 * 2);
 #pragma unroll
     for (int j = 0; j < H_PW; ++j) {
       const int row = (j * NW + wave) * RPP + lane / CPRW;
@@ -522,19 +528,11 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
       hvo[j] = ok ? (unsigned)(((long)(bimg * p.H + ih) * HWIN + iw) * p.lda * 2) + (unsigned)(((lane % CPRW) ^ swzk(row)) << 4)
                   : OOB;
     }
-#pragma unroll
-    for (int j = 0; j < BH_PW; ++j) {
-      const int row = (j * NW + wave) * RPP + lane / CPRW;
-      const int n = n0 + row;
-      bvo[j] = (j * NW + wave < HB_INS && n < p.N)
-                   ? (unsigned)((long)n * p.ldw * 2) + (unsigned)(((lane % CPRW) ^ swzk(row)) << 4) : OOB;
-    }
-#pragma unroll
-    for (int j = 0; j < A2_PW; ++j) {
-      const int row = (j * NW + wave) * RPP + lane / CPRW;
-      const int m = m0 + row;
-      a2vo[j] = (p.A2 && j * NW + wave < A2_INS && m < p.M)
-                    ? (unsigned)((long)m * p.lda2 * 2) + (unsigned)(((lane % CPRW) ^ swzk(row)) << 4) : OOB;
+    static_assert(NW * RPP % 8 == 0, "a piece round keeps the row swizzle");
+    {  // (N is a multiple of 320 and M of BM on the halo path: every issued piece is in range)
+      const int row = wave * RPP + lane / CPRW;
+      bvo0 = (unsigned)((long)(n0 + row) * p.ldw * 2) + (unsigned)(((lane % CPRW) ^ swzk(row)) << 4);
+      a2vo0 = p.A2 ? (unsigned)((long)(m0 + row) * p.lda2 * 2) + (unsigned)(((lane % CPRW) ^ swzk(row)) << 4) : OOB;
     }
     char* const hbase = smem;
     char* const bbase = smem + 2 * HBYTES;
@@ -545,15 +543,17 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
     const int nkl = 9 * nsl + n2;
     auto issue_halo = [&](int c32, int hb) {  // input channels 32 c32 .. +31 of the halo, into buffer hb
 #pragma unroll
-      for (int j = 0; j < H_PW; ++j)
-        if (j * NW + wave < H_INS) bld16(rsA, hbase + hb * HBYTES + (j * NW + wave) * 1024, hvo[j], (unsigned)(c32 * 64));
+      for (int j = 0; j < H_PW; ++j)  // (whole rounds of pieces need no per-wave test)
+        if ((j + 1) * NW <= H_INS || j * NW + wave < H_INS)
+          bld16(rsA, hbase + hb * HBYTES + (j * NW + wave) * 1024, hvo[j], (unsigned)(c32 * 64));
     };
     // B tiles: a 4-slot ring (slot ks % 4), issued three local K-steps ahead; A2 tiles (folded shortcut): three slots
     // in the halo buffers (slot ks % 3), issued two steps ahead, ahead of the B tile issued at the same point
     auto issue_b_kb = [&](int ks, unsigned kb) {
 #pragma unroll
       for (int j = 0; j < BH_PW; ++j)
-        if (j * NW + wave < HB_INS) bld16(rsW, bbase + (ks & 3) * BSTAGE + (j * NW + wave) * 1024, bvo[j], kb);
+        if ((j + 1) * NW <= HB_INS || j * NW + wave < HB_INS)
+          bld16(rsW, bbase + (ks & 3) * BSTAGE + (j * NW + wave) * 1024, bvo0, kb + j * bstep);
     };
     // W columns of main slice c32 (global 32-channel slice) at tap: ((c32 / 2) * 9 + tap) * 64 + (c32 % 2) * 32; of
     // shortcut step k2 (local): 9 Cin + 32 (k2_first + k2)
@@ -568,7 +568,8 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
       const int k2 = k2_first + ks - 9 * nsl;
 #pragma unroll
       for (int j = 0; j < A2_PW; ++j)
-        if (j * NW + wave < A2_INS) bld16(rsA2, a2s + (j * NW + wave) * 1024, a2vo[j], (unsigned)(64 * k2));
+        if ((j + 1) * NW <= A2_INS || j * NW + wave < A2_INS)
+          bld16(rsA2, a2s + (j * NW + wave) * 1024, a2vo0, (unsigned)(64 * k2) + j * a2step);
     };
     auto vm_wait = [&](int n) {  // s_waitcnt vmcnt(n) for the wave-uniform n (immediates only; smaller = safe)
       if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
@@ -690,105 +691,127 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
         a1 = n1;
       }
     };
-    if (nkl > 0) {
-      if (nsl > 0) issue_halo(c_first, 0);
-      if (!(p.diag & 1)) {  // points -3, -2, -1: B(0); A2(0), B(1); A2(1), B(2)
-        issue_b_any(0);
-        if (is_sc(0)) issue_a2(0);
-        if (nkl > 1) issue_b_any(1);
-        if (is_sc(1)) issue_a2(1);
-        if (nkl > 2) issue_b_any(2);
-      }
-      // younger than B(0): A2(0), B(1), A2(1), B(2)
-      const int w0 = (is_sc(0) ? a2_cnt : 0) + (nkl > 1 ? b_cnt : 0) + (is_sc(1) ? a2_cnt : 0) + (nkl > 2 ? b_cnt : 0);
-      if (gn && nsl > 0) {  // the first slice's halo (the oldest load) landed, visible to all, normalised
-        vm_wait(w0 + b_cnt);
+    // Every main slice but the last has a successor (MORE), so its taps' waits are compile-time counts; the last slice
+    // and the shortcut steps count at run time. The diagnostics knob is read here only in an SDMOE_GEMM_DIAG build
+    // (make DIAG=1): its per-step tests cost the production loop branches. (A second, diagnostics-reading copy of the
+    // loop pushed the 256x320 tiles past 256 VGPRs into scratch.) The compile-time waits
+    // use the smallest per-wave piece counts (b_lo, h_lo): a wave holding one more piece waits for that piece too --
+    // issued a full K-step earlier -- instead of walking a compare-and-branch chain for its exact count every step.
+    constexpr int b_lo = HB_INS / NW, h_lo = H_INS / NW;
+    auto main_loop = [&](auto diag_tag) {
+      constexpr bool DG = decltype(diag_tag)::value;
+      const int diag = DG ? p.diag : 0;  // (0: every diagnostics test below folds away)
+      if (nkl > 0) {
+        if (nsl > 0) issue_halo(c_first, 0);
+        if (!(diag & 1)) {  // points -3, -2, -1: B(0); A2(0), B(1); A2(1), B(2)
+          issue_b_any(0);
+          if (is_sc(0)) issue_a2(0);
+          if (nkl > 1) issue_b_any(1);
+          if (is_sc(1)) issue_a2(1);
+          if (nkl > 2) issue_b_any(2);
+        }
+        // younger than B(0): A2(0), B(1), A2(1), B(2)
+        const int w0 = (is_sc(0) ? a2_cnt : 0) + (nkl > 1 ? b_cnt : 0) + (is_sc(1) ? a2_cnt : 0) + (nkl > 2 ? b_cnt : 0);
+        if (gn && nsl > 0) {  // the first slice's halo (the oldest load) landed, visible to all, normalised
+          vm_wait(w0 + b_cnt);
+          __syncthreads();
+          transform(c_first, 0);
+        }
+        vm_wait(w0);
         __syncthreads();
-        transform(c_first, 0);
+        read_b(0);
+        if (nsl > 0) {
+          a0 = a_frag(hbase + hrow, std::integral_constant<int, 0>(), 0);
+          a1 = a_frag(hbase + hrow, std::integral_constant<int, 0>(), 1);
+        }
       }
-      vm_wait(w0);
-      __syncthreads();
-      read_b(0);
-      if (nsl > 0) {
-        a0 = a_frag(hbase + hrow, std::integral_constant<int, 0>(), 0);
-        a1 = a_frag(hbase + hrow, std::integral_constant<int, 0>(), 1);
-      }
-    }
-    for (int cs = 0; cs < nsl; ++cs) {
-      const bool more = cs + 1 < nsl;
-      const char* const hcur = hbase + (cs & 1) * HBYTES + hrow;
-      const char* const hnxt = hbase + ((cs & 1) ^ 1) * HBYTES + hrow;
-      const int c32 = c_first + cs;
-      auto tap_step = [&](auto tc) {
-        constexpr int t = decltype(tc)::value;
-        const int ks = cs * 9 + t;
-        // younger than B(ks + 1): the halo issued at point ks - 2 (t == 2) and ks - 1 (t == 1), A2(ks + 1) (the
-        // first shortcut step, t == 8 of the last slice), B(ks + 2)
-        int nwait = ks + 2 < nkl ? b_cnt : 0;
-        if ((t == 1 || t == 2) && more) nwait += h_cnt;
-        if (t == 8 && !more && n2 > 0) nwait += a2_cnt;
-        vm_wait(ks + 1 < nkl ? nwait : 0);
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        if (t == 5 && more && gn) transform(c32 + 1, (cs & 1) ^ 1);
-        auto mid = [&]() {
-          if (p.diag & 1) return;
-          if (t >= 7 && !more && n2 > t - 7) issue_a2(ks + 2);  // A2 of shortcut step t - 7
-          if constexpr (t + 3 < 9) {
-            issue_b_kb(ks + 3, kb_main(c32, t + 3));
+      auto slice = [&](int cs, auto more_tag) {
+        constexpr bool MORE = decltype(more_tag)::value;
+        const char* const hcur = hbase + (cs & 1) * HBYTES + hrow;
+        const char* const hnxt = hbase + ((cs & 1) ^ 1) * HBYTES + hrow;
+        const int c32 = c_first + cs;
+        auto tap_step = [&](auto tc) {
+          constexpr int t = decltype(tc)::value;
+          const int ks = cs * 9 + t;
+          // younger than B(ks + 1): the halo issued at point ks - 2 (t == 2) and ks - 1 (t == 1), A2(ks + 1) (the
+          // first shortcut step, t == 8 of the last slice), B(ks + 2)
+          if constexpr (MORE) {
+            vm_wait(b_lo + ((t == 1 || t == 2) ? h_lo : 0));
           } else {
-            if (more) issue_b_kb(ks + 3, kb_main(c32 + 1, t - 6));
-            else if (n2 > t - 6) issue_b_kb(ks + 3, kb_sc(t - 6));
+            int nwait = ks + 2 < nkl ? b_cnt : 0;
+            if (t == 8 && n2 > 0) nwait += a2_cnt;
+            vm_wait(ks + 1 < nkl ? nwait : 0);
           }
-          if (t == 0 && more) issue_halo(c32 + 1, (cs & 1) ^ 1);
-        };
-        if (!(p.diag & 2)) mfma_groups([&](int i) -> half8 { return a_frag(hcur, tc, i); }, mid);
-        else mid();
-        // read-ahead of step ks + 1: tap t + 1, or tap 0 of the next slice, or (B only) the first shortcut step
-        if constexpr (t < 8) {
-          read_b(ks + 1);
-          a0 = a_frag(hcur, std::integral_constant<int, t + 1>(), 0);
-          a1 = a_frag(hcur, std::integral_constant<int, t + 1>(), 1);
-        } else {
-          if (ks + 1 < nkl) read_b(ks + 1);
-          if (more) {
+          __builtin_amdgcn_s_barrier();
+          asm volatile("" ::: "memory");
+          if constexpr (MORE && t == 5) {
+            if (gn) transform(c32 + 1, (cs & 1) ^ 1);
+          }
+          auto mid = [&]() {
+            if (diag & 1) return;
+            if constexpr (!MORE) {
+              if (t >= 7 && n2 > t - 7) issue_a2(ks + 2);  // A2 of shortcut step t - 7
+            }
+            if constexpr (t + 3 < 9) {
+              issue_b_kb(ks + 3, kb_main(c32, t + 3));
+            } else if constexpr (MORE) {
+              issue_b_kb(ks + 3, kb_main(c32 + 1, t - 6));
+            } else {
+              if (n2 > t - 6) issue_b_kb(ks + 3, kb_sc(t - 6));
+            }
+            if constexpr (MORE && t == 0) issue_halo(c32 + 1, (cs & 1) ^ 1);
+          };
+          if (!(diag & 2)) mfma_groups([&](int i) -> half8 { return a_frag(hcur, tc, i); }, mid);
+          else mid();
+          // read-ahead of step ks + 1: tap t + 1, or tap 0 of the next slice, or (B only) the first shortcut step
+          if constexpr (t < 8) {
+            read_b(ks + 1);
+            a0 = a_frag(hcur, std::integral_constant<int, t + 1>(), 0);
+            a1 = a_frag(hcur, std::integral_constant<int, t + 1>(), 1);
+          } else if constexpr (MORE) {
+            read_b(ks + 1);
             a0 = a_frag(hnxt, std::integral_constant<int, 0>(), 0);
             a1 = a_frag(hnxt, std::integral_constant<int, 0>(), 1);
+          } else {
+            if (ks + 1 < nkl) read_b(ks + 1);
           }
+        };
+        tap_step(std::integral_constant<int, 0>());
+        tap_step(std::integral_constant<int, 1>());
+        tap_step(std::integral_constant<int, 2>());
+        tap_step(std::integral_constant<int, 3>());
+        tap_step(std::integral_constant<int, 4>());
+        tap_step(std::integral_constant<int, 5>());
+        tap_step(std::integral_constant<int, 6>());
+        tap_step(std::integral_constant<int, 7>());
+        tap_step(std::integral_constant<int, 8>());
+      };
+      for (int cs = 0; cs + 1 < nsl; ++cs) slice(cs, std::true_type());
+      if (nsl > 0) slice(nsl - 1, std::false_type());
+      for (int k2l = 0; k2l < n2; ++k2l) {  // folded shortcut K-steps: B read ahead, the A2 pair right behind the barrier
+        const int ks = 9 * nsl + k2l;
+        // younger than B(ks + 1): A2(ks + 1), B(ks + 2)
+        vm_wait(ks + 1 < nkl ? (is_sc(ks + 1) ? a2_cnt : 0) + (ks + 2 < nkl ? b_cnt : 0) : 0);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        auto mid = [&]() {
+          if (diag & 1) return;
+          if (is_sc(ks + 2)) issue_a2(ks + 2);
+          if (ks + 3 < nkl) issue_b_kb(ks + 3, kb_sc(k2l + 3));
+        };
+        const char* a2s = a2_slot(ks) + wr * WM * RB;
+        auto a2_at = [&](int i) -> half8 { return *reinterpret_cast<const half8*>(a2s + boff + 16 * i * RB); };
+        if (!(diag & 2)) {
+          a0 = a2_at(0);
+          a1 = a2_at(1);
+          mfma_groups(a2_at, mid);
+        } else {
+          mid();
         }
-      };
-      tap_step(std::integral_constant<int, 0>());
-      tap_step(std::integral_constant<int, 1>());
-      tap_step(std::integral_constant<int, 2>());
-      tap_step(std::integral_constant<int, 3>());
-      tap_step(std::integral_constant<int, 4>());
-      tap_step(std::integral_constant<int, 5>());
-      tap_step(std::integral_constant<int, 6>());
-      tap_step(std::integral_constant<int, 7>());
-      tap_step(std::integral_constant<int, 8>());
-    }
-    for (int k2l = 0; k2l < n2; ++k2l) {  // folded shortcut K-steps: B read ahead, the A2 pair right behind the barrier
-      const int ks = 9 * nsl + k2l;
-      // younger than B(ks + 1): A2(ks + 1), B(ks + 2)
-      vm_wait(ks + 1 < nkl ? (is_sc(ks + 1) ? a2_cnt : 0) + (ks + 2 < nkl ? b_cnt : 0) : 0);
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      auto mid = [&]() {
-        if (p.diag & 1) return;
-        if (is_sc(ks + 2)) issue_a2(ks + 2);
-        if (ks + 3 < nkl) issue_b_kb(ks + 3, kb_sc(k2l + 3));
-      };
-      const char* a2s = a2_slot(ks) + wr * WM * RB;
-      auto a2_at = [&](int i) -> half8 { return *reinterpret_cast<const half8*>(a2s + boff + 16 * i * RB); };
-      if (!(p.diag & 2)) {
-        a0 = a2_at(0);
-        a1 = a2_at(1);
-        mfma_groups(a2_at, mid);
-      } else {
-        mid();
+        if (ks + 1 < nkl) read_b(ks + 1);
       }
-      if (ks + 1 < nkl) read_b(ks + 1);
-    }
+    };
+    main_loop(std::true_type());
   } else {
   // prologue: stages 0 .. NSTAGE-2
 #pragma unroll
