@@ -37,9 +37,6 @@ int g_mfast = 1;   // knob 14: split-K conv grids ordered M-tile fastest (1) or 
 int g_epi_direct = 1;
 int g_cus = 256;  // compute units of the device (device_cus(): hipDeviceAttributeMultiprocessorCount, queried once)
 bool g_cus_init = false;
-#ifndef SDMOE_GEMM_DIAG
-#define SDMOE_GEMM_DIAG 0  // 1: the halo conv loop honours the diagnostics knob too (make DIAG=1)
-#endif
 int g_diag = 0;  // knob 6, diagnostics only (results garbage): bit 0 = no K-loop operand loads, bit 1 = no MFMAs,
                  // bit 4 = no A-operand pieces, bit 5 = no B-operand pieces,
                  // bit 2 = no epilogue (nothing stored), bit 3 = epilogue without its global stores
@@ -692,15 +689,13 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
       }
     };
     // Every main slice but the last has a successor (MORE), so its taps' waits are compile-time counts; the last slice
-    // and the shortcut steps count at run time. The diagnostics knob is read here only in an SDMOE_GEMM_DIAG build
-    // (make DIAG=1): its per-step tests cost the production loop branches. (A second, diagnostics-reading copy of the
-    // loop pushed the 256x320 tiles past 256 VGPRs into scratch.) The compile-time waits
+    // and the shortcut steps count at run time. (The diagnostics knob stays a run-time test: a copy of the loop with it
+    // compile-time off pushed the 256x320 tiles to 256 VGPRs + 188 B of scratch.) The compile-time waits
     // use the smallest per-wave piece counts (b_lo, h_lo): a wave holding one more piece waits for that piece too --
     // issued a full K-step earlier -- instead of walking a compare-and-branch chain for its exact count every step.
     constexpr int b_lo = HB_INS / NW, h_lo = H_INS / NW;
-    auto main_loop = [&](auto diag_tag) {
-      constexpr bool DG = decltype(diag_tag)::value;
-      const int diag = DG ? p.diag : 0;  // (0: every diagnostics test below folds away)
+    auto main_loop = [&]() {
+      const int diag = p.diag;
       if (nkl > 0) {
         if (nsl > 0) issue_halo(c_first, 0);
         if (!(diag & 1)) {  // points -3, -2, -1: B(0); A2(0), B(1); A2(1), B(2)
@@ -811,7 +806,7 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
         if (ks + 1 < nkl) read_b(ks + 1);
       }
     };
-    main_loop(std::true_type());
+    main_loop();
   } else {
   // prologue: stages 0 .. NSTAGE-2
 #pragma unroll
