@@ -45,8 +45,9 @@ def main():
     dev = "cuda"
     rows = []
     # convs: (H, Cin, Cout, stride, upsample)
-    for H, Cin, Cout, st, up in [(64, 320, 320, 1, 0), (64, 640, 320, 1, 0), (32, 640, 640, 1, 0),
-                                  (32, 1280, 640, 1, 0), (16, 1280, 1280, 1, 0), (16, 2560, 1280, 1, 0),
+    for H, Cin, Cout, st, up in [(64, 320, 320, 1, 0), (64, 640, 320, 1, 0), (64, 960, 320, 1, 0),
+                                  (32, 640, 640, 1, 0), (32, 960, 640, 1, 0), (32, 1280, 640, 1, 0),
+                                  (32, 1920, 640, 1, 0), (16, 1280, 1280, 1, 0), (16, 2560, 1280, 1, 0),
                                   (8, 1280, 1280, 1, 0), (8, 2560, 1280, 1, 0), (64, 320, 320, 2, 0),
                                   (32, 640, 640, 2, 0), (16, 1280, 1280, 2, 0),
                                   (32, 640, 640, 1, 1), (16, 1280, 1280, 1, 1), (8, 1280, 1280, 1, 1),
