@@ -732,6 +732,8 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
           // first shortcut step, t == 8 of the last slice), B(ks + 2)
           if constexpr (MORE) {
             vm_wait(b_lo + ((t == 1 || t == 2) ? h_lo : 0));
+          } else if constexpr (t <= 6) {  // last slice: B(ks + 2) is a main-slice tile up to tap 6, nothing else younger
+            vm_wait(b_lo);
           } else {
             int nwait = ks + 2 < nkl ? b_cnt : 0;
             if (t == 8 && n2 > 0) nwait += a2_cnt;
