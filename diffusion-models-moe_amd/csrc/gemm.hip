@@ -787,8 +787,9 @@ __global__ __launch_bounds__(64 * WMW * WNW, (NSTAGE == 2 && (WMW * WNW == 4 || 
       if (nsl > 0) slice(nsl - 1, std::false_type());
       for (int k2l = 0; k2l < n2; ++k2l) {  // folded shortcut K-steps: B read ahead, the A2 pair right behind the barrier
         const int ks = 9 * nsl + k2l;
-        // younger than B(ks + 1): A2(ks + 1), B(ks + 2)
-        vm_wait(ks + 1 < nkl ? (is_sc(ks + 1) ? a2_cnt : 0) + (ks + 2 < nkl ? b_cnt : 0) : 0);
+        // younger than B(ks + 1): A2(ks + 1), B(ks + 2) -- compile-time counts but for the last two steps
+        if (ks + 2 < nkl) vm_wait(A2_INS / NW + b_lo);
+        else vm_wait(ks + 1 < nkl ? (is_sc(ks + 1) ? a2_cnt : 0) + (ks + 2 < nkl ? b_cnt : 0) : 0);
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         auto mid = [&]() {
