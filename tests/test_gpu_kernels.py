@@ -368,6 +368,7 @@ def _with_tune(settings, fn):
     finally:
         _lib.check(lib.sdmoe_tune(0, 0), "tune")
         _lib.check(lib.sdmoe_tune(1, 0), "tune")
+        _lib.check(lib.sdmoe_tune(9, 0), "tune")
         _lib.check(lib.sdmoe_tune(16, 1), "tune")
         _lib.check(lib.sdmoe_tune(20, 1), "tune")
         _lib.check(lib.sdmoe_tune(21, 1), "tune")
@@ -702,6 +703,27 @@ def test_conv3x3_folded_shortcut(H, C, Cin2, nimg):
     ref = ref + x.float() @ wsc.float().t() + cadd.float().repeat_interleave(H * H, 0)
     close(out, ref)
 
+
+
+@pytest.mark.parametrize("H,C,Cin2,nimg", [(64, 320, 640, 2), (32, 640, 960, 2), (16, 1280, 2560, 2)])
+@pytest.mark.parametrize("ks", [1, 2, 3, 4, 7, 10, 20])
+def test_conv3x3_halo_forced_splits(H, C, Cin2, nimg, ks):
+    """Halo convs with the folded shortcut at forced split-K counts (sdmoe_tune knob 9): 1..20 splits leave each
+    workgroup from one to all of its 32-channel main slices and from one to all of the shortcut's steps, so every wait
+    regime of the halo loop -- compile-time counts in slices with a successor, in taps 0-6 of the last slice and in the
+    shortcut steps but the last two, run-time counts elsewhere -- runs at every slice count; vs torch fp32 (any
+    missed LDS-DMA wait reads a stale or half-landed tile: garbage, far outside the tolerance)."""
+    hn = rnd(nimg * H * H, C, seed=111 + ks)
+    x = rnd(nimg * H * H, Cin2, seed=112)
+    w = rnd(C, C, 3, 3, scale=(9 * C) ** -0.5, seed=113)
+    wsc = rnd(C, Cin2, scale=Cin2 ** -0.5, seed=114)
+    b = rnd(C, scale=0.1, seed=115)
+    wcat = ops.conv_weight_with_shortcut(ops.conv_weight_from_torch(w), wsc)
+    out = []
+    _with_tune([(9, ks)], lambda: out.append(ops.conv3x3(hn, nimg, H, H, wcat, b, shortcut=x)))
+    xi = hn.float().reshape(nimg, H, H, C).permute(0, 3, 1, 2)
+    ref = F.conv2d(xi, w.float(), b.float(), padding=1).permute(0, 2, 3, 1).reshape(-1, C)
+    close(out[0], ref + x.float() @ wsc.float().t())
 
 
 @pytest.mark.parametrize("kind", ["linear", "linear_res", "linear_ln", "conv_temb", "conv_halo_sc", "keep", "per_image"])
