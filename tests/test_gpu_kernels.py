@@ -488,6 +488,32 @@ def test_conv3x3_groupnorm_in_kernel_bit_identical(Cin, Cout, Cin2, nimg, res):
     close(fused, ref)
 
 
+@pytest.mark.parametrize("Cin,Cin2", [(320, 640), (640, 0)])
+@pytest.mark.parametrize("ks", [1, 2, 3, 7, 10])
+def test_conv3x3_groupnorm_in_kernel_forced_splits(Cin, Cin2, ks):
+    """The in-kernel GroupNorm halo conv at forced split-K counts (knob 9): the next slice is normalised at tap 5 only
+    in slices with a successor, the first in the prologue -- with 1 .. all slices per workgroup both paths run at
+    every count. Bit-identical to sdmoe_groupnorm_apply + the plain halo conv under the same split."""
+    H, nimg, Cout = 64, 2, 320
+    x = rnd(nimg * H * H, Cin, seed=Cin + ks) * 2 + 0.5
+    gamma, beta = rnd(Cin, scale=0.1, seed=11) + 1, rnd(Cin, scale=0.1, seed=12)
+    sc, sh = ops.groupnorm_stats(x, nimg, H * H, gamma, beta, 1e-5, 32)
+    w, b = rnd(Cout, 3, 3, Cin, scale=(9 * Cin) ** -0.5, seed=13), rnd(Cout, scale=0.1, seed=14)
+    if Cin2:
+        x2 = rnd(nimg * H * H, Cin2, seed=15)
+        wc = ops.conv_weight_with_shortcut(ops.conv_weight(w), rnd(Cout, Cin2, scale=Cin2 ** -0.5, seed=16))
+        kw = dict(shortcut=x2)
+    else:
+        wc, kw = ops.conv_weight(w), dict(residual=rnd(nimg * H * H, Cout, seed=17))
+    outs = []
+
+    def run():
+        outs.append(ops.conv3x3(x, nimg, H, H, wc, b, gn=(sc, sh, True), **kw))
+        outs.append(ops.conv3x3(ops.groupnorm_apply(x, nimg, H * H, sc, sh, True), nimg, H, H, wc, b, **kw))
+    _with_tune([(9, ks)], run)
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_conv3x3_full_size_upsample_concat():
     """The 32x32 -> 64x64 upsample conv (640 ch) and a 64x64 skip-concat conv input (960 -> 320) at batch 16."""
     nimg = 16
