@@ -488,6 +488,18 @@ def test_conv3x3_groupnorm_in_kernel_bit_identical(Cin, Cout, Cin2, nimg, res):
     close(fused, ref)
 
 
+@pytest.mark.parametrize("H,C,nimg", [(32, 640, 2), (16, 1280, 2), (8, 1280, 3)])
+@pytest.mark.parametrize("ks", [1, 2, 5, 20])
+def test_conv3x3_halo_upsample_forced_splits(H, C, nimg, ks):
+    """The 2x-upsample halo convs (MODE_CONVHUP*) at forced split-K counts (knob 9): 1 .. all slices per workgroup;
+    vs torch fp32 (nearest upsample, then the 3x3 conv)."""
+    x = rnd(nimg * H * H, C, seed=H + ks)
+    w, b = rnd(C, 3, 3, C, scale=(9 * C) ** -0.5, seed=H + 1), rnd(C, scale=0.1, seed=H + 2)
+    out = []
+    _with_tune([(9, ks)], lambda: out.append(ops.conv3x3(x, nimg, H, H, ops.conv_weight(w), b, upsample=True)))
+    close(out[0], conv_ref(x, nimg, H, H, w, b, 1, True))
+
+
 @pytest.mark.parametrize("Cin,Cin2", [(320, 640), (640, 0)])
 @pytest.mark.parametrize("ks", [1, 2, 3, 7, 10])
 def test_conv3x3_groupnorm_in_kernel_forced_splits(Cin, Cin2, ks):
